@@ -1,0 +1,764 @@
+// engine.cpp — the C ABI of include/bt.h: engine lifecycle, HBM-resident datasets, the
+// JobsReply batch entry point (drop-in for process_incoming_job,
+// /root/reference/src/worker/process.rs:13-29) and result serialisation.
+//
+// Nothing here computes a backtest on the CPU: every result comes from the HIP kernels in
+// k_*.hip. The host parses CSV bytes (ingest), moves bars to HBM, launches, and formats
+// CompleteRequest.data strings (/root/reference/proto/backtesting.proto:29-32).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "csv.h"
+#include "internal.h"
+
+using namespace bt;
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+struct HipFail {
+    std::string msg;
+};
+
+#define HIPCHK(x)                                                                              \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess)                                                                  \
+            throw HipFail{std::string(#x) + ": " + hipGetErrorString(e_)};                     \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t want) {
+        if (want <= n && p) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (want == 0) return;
+        HIPCHK(hipMalloc(&p, want * sizeof(T)));
+        n = want;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+uint32_t next_pow2(uint32_t x) {
+    uint32_t r = 1;
+    while (r < x) r <<= 1;
+    return r;
+}
+
+}  // namespace
+
+struct bt_engine {
+    bt_config cfg{};
+    std::vector<int32_t> ax[4];  // owned copies of the grid axes
+    Grid grid{};
+    int32_t P = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    DevBuf<int32_t> d_axes[4];
+    // dataset
+    std::vector<SymDesc> syms;
+    int64_t rows = 0;
+    DevBuf<SymDesc> d_syms;
+    DevBuf<int32_t> d_c, d_h, d_l;
+    DevBuf<int64_t> d_q, d_q2;
+    // outputs
+    DevBuf<bt_summary> d_sum;
+    DevBuf<uint64_t> d_key;
+    DevBuf<bt_sums> d_sums;
+    DevBuf<bt_trade> d_trades;
+    DevBuf<unsigned long long> d_ntr;
+    // top-k work
+    DevBuf<unsigned int> d_hist, d_counts;
+    DevBuf<unsigned long long> d_state, d_above, d_equal;
+    bool ran = false;
+    // timing of the dominant kernel
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
+    double kernel_ms = 0.0;
+    int64_t launches = 0;
+};
+
+namespace {
+
+void activate(bt_engine* e) { HIPCHK(hipSetDevice(e->cfg.device)); }
+
+bool has_hl(const bt_engine* e) { return e->cfg.strategy == BT_BOLL; }
+
+const char* kernel_name(int32_t strategy) {
+    switch (strategy) {
+        case BT_SMA_CROSS: return "bt::sma_kernel";
+        case BT_EMA_OLS: return "bt::ema_ols_kernel";
+        default: return "bt::boll_kernel";
+    }
+}
+
+std::string validate_and_copy(bt_engine* e, const bt_config& c) {
+    auto copy_axis = [&](int slot, const int32_t* src, int32_t n, const char* what, int32_t lo,
+                         int32_t hi) -> std::string {
+        if (n <= 0 || src == nullptr) return std::string("empty axis: ") + what;
+        e->ax[slot].assign(src, src + n);
+        for (int32_t v : e->ax[slot])
+            if (v < lo || v > hi)
+                return std::string("value out of range on axis ") + what + ": " + std::to_string(v);
+        return "";
+    };
+    std::string err;
+    e->grid.strategy = c.strategy;
+    switch (c.strategy) {
+        case BT_SMA_CROSS: {
+            if (!(err = copy_axis(0, c.fast, c.n_fast, "fast", 1, kMaxBars)).empty()) return err;
+            if (!(err = copy_axis(1, c.slow, c.n_slow, "slow", 1, kMaxBars)).empty()) return err;
+            const int64_t mf = *std::max_element(e->ax[0].begin(), e->ax[0].end());
+            const int64_t ms = *std::max_element(e->ax[1].begin(), e->ax[1].end());
+            // exact key comparison needs fast*slow < 2^21 (see k_sma.hip)
+            if (mf * ms >= (1LL << 21)) return "SMA grid outside the exact-key range (max fast*slow >= 2^21)";
+            e->grid.na = c.n_fast;
+            e->grid.nb = c.n_slow;
+            e->grid.nc = e->grid.nd = 1;
+            e->grid.wmax = (int32_t)std::max(mf, ms);
+            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + kTile);
+            const size_t nw = (size_t)c.n_fast + c.n_slow;
+            const size_t lds = (size_t)e->grid.ring * 8 + ((nw * (kTile + 1) * 8 + 15) & ~size_t(15)) +
+                               6 * kTile * 16 + 4 * kTile * 8 + kTile * 4 + nw * 4;
+            if (lds > 160 * 1024) return "SMA grid needs more LDS than a CU has (windows too long)";
+            break;
+        }
+        case BT_EMA_OLS: {
+            if (!(err = copy_axis(0, c.span, c.n_span, "span", 1, kMaxBars)).empty()) return err;
+            if (!(err = copy_axis(1, c.ols, c.n_ols, "ols", 1, 1 << 16)).empty()) return err;
+            if (c.band_bps < 0 || c.band_bps >= 10000) return "band_bps out of range";
+            e->grid.na = c.n_span;
+            e->grid.nb = c.n_ols;
+            e->grid.nc = e->grid.nd = 1;
+            e->grid.band_bps = c.band_bps;
+            break;
+        }
+        case BT_BOLL: {
+            if (!(err = copy_axis(0, c.bwin, c.n_bwin, "bwin", 1, 1 << 16)).empty()) return err;
+            if (!(err = copy_axis(1, c.k_num, c.n_k, "k_num", 0, 1 << 20)).empty()) return err;
+            if (!(err = copy_axis(2, c.sl_bps, c.n_sl, "sl_bps", 0, 9999)).empty()) return err;
+            if (!(err = copy_axis(3, c.tp_bps, c.n_tp, "tp_bps", 0, 9999)).empty()) return err;
+            if (c.k_den < 1 || c.k_den > (1 << 20)) return "k_den out of range";
+            e->grid.na = c.n_bwin;
+            e->grid.nb = c.n_k;
+            e->grid.nc = c.n_sl;
+            e->grid.nd = c.n_tp;
+            e->grid.k_den = c.k_den;
+            break;
+        }
+        default:
+            return "unknown strategy";
+    }
+    const int64_t P = (int64_t)e->grid.na * e->grid.nb * e->grid.nc * e->grid.nd;
+    if (P <= 0 || P > (1 << 20)) return "parameter grid too large";
+    e->P = (int32_t)P;
+    e->grid.n_params = e->P;
+    if (c.annualization <= 0) return "annualization must be positive";
+    e->grid.sqrt_ann = std::sqrt((double)c.annualization);
+    if (c.topk < 0) return "topk must be >= 0";
+    if ((c.flags & BT_FLAG_PARITY) && c.trade_cap <= 0) return "parity mode needs trade_cap > 0";
+    return "";
+}
+
+void upload_grid(bt_engine* e) {
+    const int32_t** dst[4] = {&e->grid.a, &e->grid.b, &e->grid.c, &e->grid.d};
+    for (int i = 0; i < 4; ++i) {
+        *dst[i] = nullptr;
+        if (e->ax[i].empty()) continue;
+        e->d_axes[i].ensure(e->ax[i].size());
+        HIPCHK(hipMemcpy(e->d_axes[i].p, e->ax[i].data(), e->ax[i].size() * 4, hipMemcpyHostToDevice));
+        *dst[i] = e->d_axes[i].p;
+    }
+}
+
+// Lay out rows (64-element aligned) and allocate the columns the strategy needs.
+void layout(bt_engine* e, int32_t n_sym, const int32_t* bars, const int64_t* ids) {
+    e->syms.resize(n_sym);
+    int64_t off = 0;
+    for (int32_t s = 0; s < n_sym; ++s) {
+        e->syms[s].off = off;
+        e->syms[s].bars = bars[s];
+        e->syms[s].id = (int32_t)ids[s];
+        off += ((int64_t)bars[s] + kRowAlign - 1) / kRowAlign * kRowAlign;
+    }
+    e->rows = off;
+    e->d_syms.ensure(std::max<size_t>(1, n_sym));
+    if (n_sym)
+        HIPCHK(hipMemcpyAsync(e->d_syms.p, e->syms.data(), n_sym * sizeof(SymDesc),
+                              hipMemcpyHostToDevice, e->stream));
+    const size_t rows = std::max<int64_t>(1, off);
+    e->d_c.ensure(rows);
+    if (has_hl(e)) {
+        e->d_h.ensure(rows);
+        e->d_l.ensure(rows);
+    }
+    if (e->cfg.strategy != BT_SMA_CROSS) {
+        e->d_q.ensure(rows);
+        e->d_q2.ensure(rows);
+    }
+    e->ran = false;
+}
+
+void ensure_outputs(bt_engine* e) {
+    const size_t n = (size_t)e->syms.size() * e->P;
+    e->d_sum.ensure(std::max<size_t>(1, n));
+    e->d_key.ensure(std::max<size_t>(1, n));
+    e->d_ntr.ensure(1);
+    if (e->cfg.flags & BT_FLAG_PARITY) {
+        e->d_sums.ensure(std::max<size_t>(1, n));
+        e->d_trades.ensure(std::max<size_t>(1, n * (size_t)e->cfg.trade_cap));
+    }
+    if (e->cfg.topk > 0) {
+        e->d_hist.ensure(256);
+        e->d_counts.ensure(2);
+        e->d_state.ensure(4);
+        e->d_above.ensure(std::max<size_t>(1, n));
+        e->d_equal.ensure(std::max<size_t>(1, n));
+    }
+}
+
+void run_impl(bt_engine* e) {
+    activate(e);
+    ensure_outputs(e);
+    const int32_t S = (int32_t)e->syms.size();
+    Out out{};
+    out.sum = e->d_sum.p;
+    out.key = e->d_key.p;
+    const bool parity = (e->cfg.flags & BT_FLAG_PARITY) != 0;
+    out.sums = parity ? e->d_sums.p : nullptr;
+    out.trades = parity ? e->d_trades.p : nullptr;
+    out.trade_cap = parity ? e->cfg.trade_cap : 0;
+    out.n_trades = e->d_ntr.p;
+    HIPCHK(hipMemsetAsync(e->d_ntr.p, 0, sizeof(unsigned long long), e->stream));
+    const bool timing = (e->cfg.flags & BT_FLAG_TIMING) != 0;
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (timing) {
+        if (!e->ev_pool.empty()) {
+            ev = e->ev_pool.back();
+            e->ev_pool.pop_back();
+        } else {
+            HIPCHK(hipEventCreate(&ev.first));
+            HIPCHK(hipEventCreate(&ev.second));
+        }
+        HIPCHK(hipEventRecord(ev.first, e->stream));
+    }
+    hipError_t err = hipSuccess;
+    switch (e->cfg.strategy) {
+        case BT_SMA_CROSS:
+            err = launch_sma(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
+            break;
+        case BT_EMA_OLS:
+            err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->d_q.p, e->d_q2.p, e->grid, out, parity,
+                                 e->stream);
+            break;
+        case BT_BOLL:
+            err = launch_boll(e->d_syms.p, S, e->d_h.p, e->d_l.p, e->d_c.p, e->d_q.p, e->d_q2.p,
+                              e->grid, out, parity, e->stream);
+            break;
+    }
+    HIPCHK(err);
+    if (timing) {
+        HIPCHK(hipEventRecord(ev.second, e->stream));
+        e->ev_pending.push_back(ev);
+    }
+    if (e->cfg.topk > 0) {
+        TopkWork w{e->d_hist.p, e->d_state.p, e->d_counts.p, e->d_above.p, e->d_equal.p};
+        HIPCHK(launch_topk(e->d_key.p, (int64_t)S * e->P, e->cfg.topk, w, e->stream));
+    }
+    e->ran = true;
+}
+
+void drain_timing(bt_engine* e) {
+    for (auto& ev : e->ev_pending) {
+        HIPCHK(hipEventSynchronize(ev.second));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
+        e->kernel_ms += ms;
+        e->launches += 1;
+        e->ev_pool.push_back(ev);
+    }
+    e->ev_pending.clear();
+}
+
+bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b) {  // "a ranks before b"
+    const uint64_t ka = order_key(a.sharpe), kb = order_key(b.sharpe);
+    if (ka != kb) return ka > kb;
+    if (a.sym != b.sym) return a.sym < b.sym;
+    return a.param < b.param;
+}
+
+std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
+    std::vector<bt_topk_rec> res;
+    if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
+    HIPCHK(hipStreamSynchronize(e->stream));
+    unsigned int counts[2];
+    unsigned long long state[4];
+    HIPCHK(hipMemcpy(counts, e->d_counts.p, sizeof counts, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(state, e->d_state.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> idx(counts[0] + counts[1]);
+    if (counts[0])
+        HIPCHK(hipMemcpy(idx.data(), e->d_above.p, counts[0] * 8ULL, hipMemcpyDeviceToHost));
+    if (counts[1])
+        HIPCHK(hipMemcpy(idx.data() + counts[0], e->d_equal.p, counts[1] * 8ULL, hipMemcpyDeviceToHost));
+    std::vector<bt_summary> rec(1);
+    for (unsigned long long i : idx) {
+        HIPCHK(hipMemcpy(rec.data(), e->d_sum.p + i, sizeof(bt_summary), hipMemcpyDeviceToHost));
+        const int32_t s = (int32_t)(i / e->P), p = (int32_t)(i % e->P);
+        res.push_back(bt_topk_rec{rec[0].sharpe, e->syms[s].id, p, rec[0].pnl});
+    }
+    std::sort(res.begin(), res.end(), topk_less);
+    if ((int32_t)res.size() > k) res.resize(k);
+    return res;
+}
+
+std::string fmt_job(const bt_summary* r, int32_t P) {
+    std::string s;
+    s.reserve((size_t)P * 110);
+    char line[256];
+    for (int32_t p = 0; p < P; ++p) {
+        const bt_summary& x = r[p];
+        int n = snprintf(line, sizeof line,
+                         "{\"param\":%d,\"n\":%d,\"pnl\":%lld,\"mdd\":%lld,\"exp\":%lld,"
+                         "\"sharpe\":\"%.17g\",\"h\":\"%016llx\"}\n",
+                         p, x.n_trades, (long long)x.pnl, (long long)x.mdd,
+                         (long long)x.exposure, x.sharpe, (unsigned long long)x.hash);
+        s.append(line, (size_t)n);
+    }
+    return s;
+}
+
+std::string json_escape(const std::string& in) {
+    std::string o;
+    for (char ch : in) {
+        if (ch == '"' || ch == '\\') {
+            o.push_back('\\');
+            o.push_back(ch);
+        } else if ((unsigned char)ch < 0x20) {
+            o.push_back(' ');
+        } else {
+            o.push_back(ch);
+        }
+    }
+    return o;
+}
+
+char* dup_string(const std::string& s) {
+    char* p = (char*)malloc(s.size() + 1);
+    if (!p) throw std::bad_alloc();
+    memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    return p;
+}
+
+#define ABI_GUARD(fail, ...)                                   \
+    try {                                                      \
+        __VA_ARGS__                                            \
+    } catch (const HipFail& f) {                               \
+        set_err(f.msg);                                        \
+        return fail;                                           \
+    } catch (const std::exception& x) {                        \
+        set_err(std::string("exception: ") + x.what());        \
+        return fail;                                           \
+    } catch (...) {                                            \
+        set_err("unknown exception");                          \
+        return fail;                                           \
+    }
+
+}  // namespace
+
+extern "C" {
+
+int32_t bt_abi_version(void) { return BT_ABI_VERSION; }
+
+const char* bt_last_error(void) { return g_err.c_str(); }
+
+bt_engine* bt_engine_create(const bt_config* cfg, char* err, size_t errlen) {
+    auto fail = [&](const std::string& m) -> bt_engine* {
+        set_err(m);
+        if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
+        return nullptr;
+    };
+    if (cfg == nullptr) return fail("null config");
+    bt_engine* e = nullptr;
+    try {
+        e = new bt_engine();
+        e->cfg = *cfg;
+        std::string m = validate_and_copy(e, *cfg);
+        if (!m.empty()) {
+            delete e;
+            return fail(m);
+        }
+        e->cfg.fast = e->cfg.slow = e->cfg.span = e->cfg.ols = nullptr;
+        e->cfg.bwin = e->cfg.k_num = e->cfg.sl_bps = e->cfg.tp_bps = nullptr;
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (cfg->device < 0 || cfg->device >= ndev)
+            throw HipFail{"HIP device " + std::to_string(cfg->device) + " not present (" +
+                          std::to_string(ndev) + " visible)"};
+        activate(e);
+        if (cfg->stream) {
+            e->stream = (hipStream_t)cfg->stream;
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+            e->own_stream = true;
+        }
+        upload_grid(e);
+        return e;
+    } catch (const HipFail& f) {
+        delete e;
+        return fail(f.msg);
+    } catch (const std::exception& x) {
+        delete e;
+        return fail(std::string("exception: ") + x.what());
+    }
+}
+
+void bt_engine_destroy(bt_engine* e) {
+    if (!e) return;
+    try {
+        (void)hipSetDevice(e->cfg.device);
+        if (e->stream) (void)hipStreamSynchronize(e->stream);
+        for (auto& ev : e->ev_pending) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+        for (auto& ev : e->ev_pool) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+        for (auto& b : e->d_axes) b.release();
+        e->d_syms.release();
+        e->d_c.release();
+        e->d_h.release();
+        e->d_l.release();
+        e->d_q.release();
+        e->d_q2.release();
+        e->d_sum.release();
+        e->d_key.release();
+        e->d_sums.release();
+        e->d_trades.release();
+        e->d_ntr.release();
+        e->d_hist.release();
+        e->d_counts.release();
+        e->d_state.release();
+        e->d_above.release();
+        e->d_equal.release();
+        if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    } catch (...) {
+    }
+    delete e;
+}
+
+int32_t bt_num_params(const bt_engine* e) { return e ? e->P : -1; }
+
+int32_t bt_load_synthetic(bt_engine* e, uint64_t seed, int64_t sym_begin, int32_t n_sym,
+                          int32_t n_bars, int32_t freq) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        if (n_sym < 0 || n_bars < 1 || n_bars > kMaxBars) throw HipFail{"bad synthetic shape"};
+        if (sym_begin < 0 || sym_begin + n_sym > (1LL << 31)) throw HipFail{"bad symbol ids"};
+        if (freq != BT_DAILY && freq != BT_MINUTE) throw HipFail{"bad freq"};
+        activate(e);
+        std::vector<int32_t> bars(n_sym, n_bars);
+        std::vector<int64_t> ids(n_sym);
+        for (int32_t s = 0; s < n_sym; ++s) ids[s] = sym_begin + s;
+        layout(e, n_sym, bars.data(), ids.data());
+        HIPCHK(launch_gen(e->d_syms.p, n_sym, seed, freq, nullptr, has_hl(e) ? e->d_h.p : nullptr,
+                          has_hl(e) ? e->d_l.p : nullptr, e->d_c.p, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return 0;
+    })
+}
+
+int32_t bt_load_ohlc(bt_engine* e, int32_t n_sym, const int64_t* sym_ids, const int32_t* bars,
+                     const int64_t* row_off, const int32_t* h, const int32_t* l, const int32_t* c) {
+    ABI_GUARD(-1, {
+        if (!e || n_sym < 0 || (n_sym > 0 && (!sym_ids || !bars || !row_off || !c)))
+            throw HipFail{"bad arguments"};
+        if (has_hl(e) && (!h || !l)) throw HipFail{"strategy needs high and low columns"};
+        for (int32_t s = 0; s < n_sym; ++s)
+            if (bars[s] < 1 || bars[s] > kMaxBars) throw HipFail{"bad bar count"};
+        activate(e);
+        layout(e, n_sym, bars, sym_ids);
+        // stage through one contiguous host buffer per column with the device row layout
+        std::vector<int32_t> tmp((size_t)std::max<int64_t>(1, e->rows));
+        auto put = [&](const int32_t* src, int32_t* dst) {
+            for (int32_t s = 0; s < n_sym; ++s)
+                memcpy(tmp.data() + e->syms[s].off, src + row_off[s], (size_t)bars[s] * 4);
+            HIPCHK(hipMemcpyAsync(dst, tmp.data(), (size_t)e->rows * 4, hipMemcpyHostToDevice,
+                                  e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+        };
+        if (e->rows > 0) {
+            put(c, e->d_c.p);
+            if (has_hl(e)) {
+                put(h, e->d_h.p);
+                put(l, e->d_l.p);
+            }
+        }
+        return 0;
+    })
+}
+
+int32_t bt_run(bt_engine* e) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        run_impl(e);
+        return 0;
+    })
+}
+
+int32_t bt_sync(bt_engine* e) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return 0;
+    })
+}
+
+int32_t bt_read_summaries(bt_engine* e, bt_summary* out, size_t n) {
+    ABI_GUARD(-1, {
+        if (!e || !e->ran) throw HipFail{"no results"};
+        const size_t have = e->syms.size() * (size_t)e->P;
+        if (n > have) throw HipFail{"n exceeds symbols x params"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d_sum.p, n * sizeof(bt_summary), hipMemcpyDeviceToHost));
+        return 0;
+    })
+}
+
+int32_t bt_read_sums(bt_engine* e, bt_sums* out, size_t n) {
+    ABI_GUARD(-1, {
+        if (!e || !e->ran || !(e->cfg.flags & BT_FLAG_PARITY)) throw HipFail{"no parity results"};
+        if (n > e->syms.size() * (size_t)e->P) throw HipFail{"n too large"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d_sums.p, n * sizeof(bt_sums), hipMemcpyDeviceToHost));
+        return 0;
+    })
+}
+
+int32_t bt_read_trades(bt_engine* e, bt_trade* out, size_t n) {
+    ABI_GUARD(-1, {
+        if (!e || !e->ran || !(e->cfg.flags & BT_FLAG_PARITY)) throw HipFail{"no parity results"};
+        if (n > e->syms.size() * (size_t)e->P * e->cfg.trade_cap) throw HipFail{"n too large"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d_trades.p, n * sizeof(bt_trade), hipMemcpyDeviceToHost));
+        return 0;
+    })
+}
+
+int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k) {
+    ABI_GUARD(-1, {
+        if (!e || !out || k <= 0) throw HipFail{"bad arguments"};
+        activate(e);
+        std::vector<bt_topk_rec> r = read_topk_impl(e, std::min(k, e->cfg.topk));
+        std::copy(r.begin(), r.end(), out);
+        return (int32_t)r.size();
+    })
+}
+
+int32_t bt_read_stats(bt_engine* e, bt_stats* out) {
+    ABI_GUARD(-1, {
+        if (!e || !out) throw HipFail{"bad arguments"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        bt_stats st{};
+        st.n_symbols = (int64_t)e->syms.size();
+        st.n_params = e->P;
+        for (const SymDesc& s : e->syms) st.bar_evals += (int64_t)s.bars * e->P;
+        if (e->ran) {
+            unsigned long long n = 0;
+            HIPCHK(hipMemcpy(&n, e->d_ntr.p, sizeof n, hipMemcpyDeviceToHost));
+            st.trades = (int64_t)n;
+        }
+        *out = st;
+        return 0;
+    })
+}
+
+int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n) {
+    ABI_GUARD(-1, {
+        if (!e || sym_index < 0 || sym_index >= (int32_t)e->syms.size()) throw HipFail{"bad symbol"};
+        const SymDesc& sd = e->syms[sym_index];
+        if (n > sd.bars) throw HipFail{"n exceeds bars"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d_c.p + sd.off, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return 0;
+    })
+}
+
+int32_t bt_kernel_timing(bt_engine* e, double* total_ms, int64_t* launches, const char** name) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        activate(e);
+        drain_timing(e);
+        if (total_ms) *total_ms = e->kernel_ms;
+        if (launches) *launches = e->launches;
+        if (name) *name = kernel_name(e->cfg.strategy);
+        return 0;
+    })
+}
+
+int32_t bt_reset_timing(bt_engine* e) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        activate(e);
+        drain_timing(e);
+        e->kernel_ms = 0.0;
+        e->launches = 0;
+        return 0;
+    })
+}
+
+int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* outs) {
+    ABI_GUARD(-1, {
+        if (!e || (n > 0 && (!jobs || !outs))) throw HipFail{"bad arguments"};
+        for (size_t i = 0; i < n; ++i) outs[i] = bt_job_out{nullptr, 0, 0, 0};
+        // 1. parse every job (host threads; the worker's single compute thread calls us,
+        //    /root/reference/src/worker/main.rs:38-42)
+        std::vector<Bars> bars(n);
+        std::vector<std::string> errs(n);
+        std::vector<char> ok(n, 0);
+        int nt = e->cfg.host_threads > 0 ? e->cfg.host_threads
+                                         : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+        nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(1, n));
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+            for (size_t i; (i = next.fetch_add(1)) < n;) {
+                try {
+                    ok[i] = parse_csv(jobs[i].file, jobs[i].len, bars[i], errs[i]) ? 1 : 0;
+                } catch (...) {
+                    errs[i] = "parse failure";
+                    ok[i] = 0;
+                }
+            }
+        };
+        if (nt <= 1) {
+            work();
+        } else {
+            std::vector<std::thread> th;
+            for (int i = 0; i < nt; ++i) th.emplace_back(work);
+            for (auto& t : th) t.join();
+        }
+        // 2. one HBM-resident batch of the good jobs
+        std::vector<int64_t> ids, offs;
+        std::vector<int32_t> nb;
+        std::vector<size_t> job_of;
+        int64_t rows = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (!ok[i]) continue;
+            ids.push_back((int64_t)job_of.size());
+            offs.push_back(rows);
+            nb.push_back((int32_t)bars[i].c.size());
+            rows += (int64_t)bars[i].c.size();
+            job_of.push_back(i);
+        }
+        if (!job_of.empty()) {
+            std::vector<int32_t> C((size_t)rows), H, L;
+            if (has_hl(e)) {
+                H.resize((size_t)rows);
+                L.resize((size_t)rows);
+            }
+            for (size_t k = 0; k < job_of.size(); ++k) {
+                const Bars& b = bars[job_of[k]];
+                memcpy(C.data() + offs[k], b.c.data(), b.c.size() * 4);
+                if (has_hl(e)) {
+                    memcpy(H.data() + offs[k], b.h.data(), b.h.size() * 4);
+                    memcpy(L.data() + offs[k], b.l.data(), b.l.size() * 4);
+                }
+            }
+            if (bt_load_ohlc(e, (int32_t)job_of.size(), ids.data(), nb.data(), offs.data(),
+                             has_hl(e) ? H.data() : nullptr, has_hl(e) ? L.data() : nullptr,
+                             C.data()) != 0)
+                throw HipFail{g_err};
+            run_impl(e);
+            HIPCHK(hipStreamSynchronize(e->stream));
+        }
+        // 3. one CompleteRequest.data string per job, in job order
+        std::vector<bt_summary> res((size_t)e->P);
+        size_t k = 0;
+        for (size_t i = 0; i < n; ++i) {
+            std::string s;
+            if (ok[i]) {
+                HIPCHK(hipMemcpy(res.data(), e->d_sum.p + k * (size_t)e->P,
+                                 (size_t)e->P * sizeof(bt_summary), hipMemcpyDeviceToHost));
+                s = fmt_job(res.data(), e->P);
+                outs[i].status = 0;
+                outs[i].n_bars = (int32_t)bars[i].c.size();
+                ++k;
+            } else {
+                s = "{\"error\":\"" + json_escape(errs[i]) + "\"}\n";
+                outs[i].status = -1;
+            }
+            outs[i].data = dup_string(s);
+            outs[i].len = s.size();
+        }
+        return 0;
+    })
+}
+
+void bt_job_out_free(bt_job_out* outs, size_t n) {
+    if (!outs) return;
+    for (size_t i = 0; i < n; ++i) {
+        free(outs[i].data);
+        outs[i].data = nullptr;
+        outs[i].len = 0;
+    }
+}
+
+int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* out) {
+    ABI_GUARD(-1, {
+        if ((n > 0 && !in) || !out || k < 0) throw HipFail{"bad arguments"};
+        std::vector<bt_topk_rec> v(in, in + n);
+        std::sort(v.begin(), v.end(), topk_less);
+        const size_t m = std::min<size_t>(v.size(), (size_t)k);
+        std::copy(v.begin(), v.begin() + m, out);
+        return (int32_t)m;
+    })
+}
+
+double bt_i128_to_double(uint64_t lo, int64_t hi) { return i128_to_double(lo, hi); }
+
+int32_t bt_parse_csv(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
+                     int32_t* c, char* err, size_t errlen) {
+    ABI_GUARD(-1, {
+        Bars b;
+        std::string m;
+        if (!parse_csv(buf, len, b, m)) {
+            if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
+            set_err(m);
+            return -1;
+        }
+        if ((int64_t)b.c.size() > cap) throw HipFail{"cap too small"};
+        if (h) memcpy(h, b.h.data(), b.h.size() * 4);
+        if (l) memcpy(l, b.l.data(), b.l.size() * 4);
+        if (c) memcpy(c, b.c.data(), b.c.size() * 4);
+        return (int32_t)b.c.size();
+    })
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// internal.h — layouts shared by the host engine (engine.cpp) and the HIP kernels (k_*.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bt.h"
+
+namespace bt {
+
+constexpr int kTile = 64;          // bars per LDS tile (one bit per bar in a 64-bit word)
+constexpr int kRowAlign = 64;      // symbol rows start on 64-element boundaries in HBM
+constexpr int kMaxBlock = 512;     // threads per workgroup (8 waves)
+
+// One symbol of the HBM-resident dataset: rows of int32 ticks at `off` in every column.
+struct SymDesc {
+    int64_t off;
+    int32_t bars;
+    int32_t id;                    // global symbol id (top-k tie-break, shard-independent)
+};
+
+// Device-side view of the parameter grid (copied once per engine).
+struct Grid {
+    int32_t strategy;
+    int32_t n_params;
+    int32_t na, nb, nc, nd;        // axis sizes (SMA: fast, slow; EMA: span, ols; BOLL: w,k,sl,tp)
+    int32_t band_bps, k_den;
+    int32_t wmax;                  // largest window of the grid (SMA ring sizing)
+    int32_t ring;                  // SMA prefix ring length (power of two >= wmax + kTile)
+    double sqrt_ann;               // sqrt((double)annualization), computed on the host
+    const int32_t* a;              // device arrays
+    const int32_t* b;
+    const int32_t* c;
+    const int32_t* d;
+};
+
+// Outputs of one run (device pointers).
+struct Out {
+    bt_summary* sum;               // [S * P]
+    uint64_t* key;                 // [S * P] top-k order key (orderable sharpe)
+    bt_sums* sums;                 // [S * P] parity mode, else nullptr
+    bt_trade* trades;              // [S * P * trade_cap] parity mode, else nullptr
+    int32_t trade_cap;
+    unsigned long long* n_trades;  // total trades (one atomic per block)
+};
+
+// Launchers (k_*.hip). All enqueue on `st` and return hipError_t.
+hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
+                      int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st);
+hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                      const Out& out, bool parity, hipStream_t st);
+// q/q2: [rows] int64 scratch for the fixed-point returns (spec §3) of every bar.
+hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close,
+                          int64_t* q, int64_t* q2, const Grid& g, const Out& out, bool parity,
+                          hipStream_t st);
+hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high,
+                       const int32_t* low, const int32_t* close, int64_t* q, int64_t* q2,
+                       const Grid& g, const Out& out, bool parity, hipStream_t st);
+
+// Top-k by radix select over `key` (n records); writes candidates, host finishes the order.
+struct TopkWork {
+    unsigned int* hist;            // [256]
+    unsigned long long* state;     // [4]: prefix, mask, remaining k, pad
+    unsigned int* counts;          // [2]: n_above, n_equal
+    unsigned long long* above;     // [n] indices with key > threshold (capacity n)
+    unsigned long long* equal;     // [n] indices with key == threshold
+};
+hipError_t launch_topk(const uint64_t* key, int64_t n, int32_t k, const TopkWork& w,
+                       hipStream_t st);
+
+// Shared host/device helpers.
+__host__ __device__ inline uint64_t order_key(double x) {
+    union { double d; uint64_t u; } v;
+    v.d = x;
+    return (v.u >> 63) ? ~v.u : (v.u | 0x8000000000000000ULL);
+}
+
+// int128 (lo, hi) -> double, round to nearest, ties to even (spec §4 conversion).
+__host__ __device__ inline double i128_to_double(uint64_t lo, int64_t hi) {
+    const bool neg = hi < 0;
+    uint64_t mh = (uint64_t)hi, ml = lo;
+    if (neg) {  // two's complement negate
+        ml = ~ml + 1;
+        mh = ~mh + (ml == 0 ? 1 : 0);
+    }
+    if (mh == 0 && ml == 0) return 0.0;
+    int lz = mh ? __builtin_clzll(mh) : 64 + __builtin_clzll(ml);
+    // normalise: leading one to bit 127
+    uint64_t nh, nl;
+    if (lz >= 64) {
+        nh = ml << (lz - 64);
+        nl = 0;
+    } else if (lz == 0) {
+        nh = mh;
+        nl = ml;
+    } else {
+        nh = (mh << lz) | (ml >> (64 - lz));
+        nl = ml << lz;
+    }
+    // top 53 bits = nh >> 11; remainder = low 11 bits of nh and all of nl
+    uint64_t mant = nh >> 11;
+    const uint64_t rem_hi = nh & 0x7FFULL;  // 11 bits
+    const uint64_t half = 0x400ULL;
+    bool up;
+    if (rem_hi > half) up = true;
+    else if (rem_hi < half) up = false;
+    else up = (nl != 0) || (mant & 1);
+    mant += up ? 1 : 0;
+    // value = mant * 2^(127 - lz - 52)
+    double r = (double)mant;  // exact: mant <= 2^53
+#ifdef __HIP_DEVICE_COMPILE__
+    r = ldexp(r, 75 - lz);
+#else
+    r = __builtin_ldexp(r, 75 - lz);
+#endif
+    return neg ? -r : r;
+}
+
+__host__ __device__ inline double sharpe_fx(uint64_t s1lo, int64_t s1hi, uint64_t s2lo,
+                                            int64_t s2hi, int32_t bars, double sqrt_ann) {
+    if (bars < 2) return 0.0;
+    const double n = (double)(bars - 1);
+    const double m = ldexp(i128_to_double(s1lo, s1hi), -56) / n;
+    const double mm = m * m;
+    const double v = ldexp(i128_to_double(s2lo, s2hi), -56) / n - mm;
+    return v > 0 ? (m / sqrt(v)) * sqrt_ann : 0.0;
+}
+
+}  // namespace bt

@@ -1,0 +1,62 @@
+// k_gen.hip — synthetic OHLCV straight into HBM (spec §1 / SURVEY A.1), one lane per symbol.
+//
+// The SplitMix64 stream is in counter form, so every draw is a pure function of
+// (seed, symbol, draw index); only the multiplicative walk is sequential along the bar axis.
+// Output rows are int32 ticks at SymDesc::off in each column (column pointers may be null).
+#include "internal.h"
+
+namespace bt {
+
+__device__ __forceinline__ uint64_t sm64(uint64_t s0, uint64_t k) {
+    uint64_t z = s0 + (k + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void gen_kernel(const SymDesc* __restrict__ syms, int32_t n_sym,
+                                                  uint64_t seed, int32_t freq, int32_t* o,
+                                                  int32_t* h, int32_t* l, int32_t* c) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_sym) return;
+    const SymDesc sd = syms[s];
+    const uint64_t s0 = seed ^ ((uint64_t)(int64_t)sd.id * 0x9E3779B97F4A7C15ULL);
+    const int64_t m = freq == BT_DAILY ? 17320 : 866;
+    const uint64_t span = (uint64_t)(2 * m + 1);
+    const uint64_t r = (uint64_t)(m / 4 + 1);
+    int64_t prev = 1000000 + (int64_t)(sm64(s0, 0) % 9000001ULL);
+    for (int t = 0; t < sd.bars; ++t) {
+        const uint64_t base = 1 + 7 * (uint64_t)t;
+        int64_t op = prev, cl = prev;
+        if (t > 0) {
+            int64_t x = (int64_t)(sm64(s0, base) % span) + (int64_t)(sm64(s0, base + 1) % span) +
+                        (int64_t)(sm64(s0, base + 2) % span) + (int64_t)(sm64(s0, base + 3) % span) -
+                        4 * m;
+            cl = prev + (x * prev) / 1000000;  // truncation toward zero
+            cl = cl < 10000 ? 10000 : cl;
+            cl = cl > 2146435072LL ? 2146435072LL : cl;  // 2^31 - 2^20
+        }
+        const size_t i = (size_t)sd.off + t;
+        if (c) c[i] = (int32_t)cl;
+        if (o) o[i] = (int32_t)op;
+        if (h || l) {
+            const int64_t hi = op > cl ? op : cl, lo = op < cl ? op : cl;
+            const int64_t hh = hi + (int64_t)(sm64(s0, base + 4) % r);
+            int64_t ll = lo - (int64_t)(sm64(s0, base + 5) % r);
+            ll = ll < 10000 ? 10000 : ll;
+            if (h) h[i] = (int32_t)hh;
+            if (l) l[i] = (int32_t)ll;
+        }
+        prev = cl;
+    }
+}
+
+hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
+                      int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st) {
+    if (n_sym <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_kernel, dim3((n_sym + 255) / 256), dim3(256), 0, st, syms, n_sym, seed,
+                       freq, o, h, l, c);
+    return hipGetLastError();
+}
+
+}  // namespace bt

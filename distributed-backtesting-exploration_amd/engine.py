@@ -1,0 +1,364 @@
+"""ctypes binding of libbt.so (include/bt.h) — the MI355X backtest engine.
+
+This is the Python face of the C ABI that replaces the reference worker's job function
+(/root/reference/src/worker/process.rs:13-29). Every result comes from the HIP kernels;
+there is no CPU fallback: if libbt.so or a GPU is missing, constructing an Engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass, field
+from typing import Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libbt.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+BT_SMA_CROSS, BT_EMA_OLS, BT_BOLL = 1, 2, 3
+BT_FLAG_PARITY, BT_FLAG_TIMING = 1, 2
+BT_DAILY, BT_MINUTE = 0, 1
+
+SUMMARY_DTYPE = np.dtype([
+    ("n_trades", "<i4"), ("status", "<i4"), ("pnl", "<i8"), ("mdd", "<i8"),
+    ("exposure", "<i8"), ("sharpe", "<f8"), ("hash", "<u8"),
+])
+SUMS_DTYPE = np.dtype([("s1_lo", "<u8"), ("s1_hi", "<i8"), ("s2_lo", "<u8"), ("s2_hi", "<i8")])
+TRADE_DTYPE = np.dtype([
+    ("entry_bar", "<i4"), ("exit_bar", "<i4"), ("side", "<i4"), ("pad", "<i4"),
+    ("entry_px", "<i8"), ("exit_px", "<i8"),
+])
+TOPK_DTYPE = np.dtype([("sharpe", "<f8"), ("sym", "<i4"), ("param", "<i4"), ("pnl", "<i8")])
+assert SUMMARY_DTYPE.itemsize == 48 and TOPK_DTYPE.itemsize == 24 and TRADE_DTYPE.itemsize == 32
+
+
+class BtError(RuntimeError):
+    pass
+
+
+class _Config(C.Structure):
+    _fields_ = [
+        ("strategy", C.c_int32),
+        ("n_fast", C.c_int32), ("n_slow", C.c_int32),
+        ("fast", C.POINTER(C.c_int32)), ("slow", C.POINTER(C.c_int32)),
+        ("n_span", C.c_int32), ("n_ols", C.c_int32),
+        ("span", C.POINTER(C.c_int32)), ("ols", C.POINTER(C.c_int32)),
+        ("band_bps", C.c_int32),
+        ("n_bwin", C.c_int32), ("n_k", C.c_int32), ("n_sl", C.c_int32), ("n_tp", C.c_int32),
+        ("bwin", C.POINTER(C.c_int32)), ("k_num", C.POINTER(C.c_int32)),
+        ("k_den", C.c_int32),
+        ("sl_bps", C.POINTER(C.c_int32)), ("tp_bps", C.POINTER(C.c_int32)),
+        ("annualization", C.c_int64),
+        ("device", C.c_int32), ("topk", C.c_int32), ("flags", C.c_int32),
+        ("host_threads", C.c_int32), ("trade_cap", C.c_int32),
+        ("stream", C.c_void_p),
+    ]
+
+
+class _JobIn(C.Structure):
+    _fields_ = [("id", C.c_char_p), ("file", C.c_void_p), ("len", C.c_size_t)]
+
+
+class _JobOut(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("len", C.c_size_t), ("status", C.c_int32),
+                ("n_bars", C.c_int32)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("n_symbols", C.c_int64), ("n_params", C.c_int64), ("bar_evals", C.c_int64),
+                ("trades", C.c_int64), ("errors", C.c_int64)]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libbt.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-j8", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BtError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    L.bt_engine_create.argtypes = [C.POINTER(_Config), C.c_char_p, C.c_size_t]
+    L.bt_engine_create.restype = P
+    L.bt_engine_destroy.argtypes = [P]
+    L.bt_engine_destroy.restype = None
+    L.bt_last_error.restype = C.c_char_p
+    L.bt_abi_version.restype = C.c_int32
+    L.bt_num_params.argtypes = [P]
+    L.bt_run_batch.argtypes = [P, C.c_size_t, C.POINTER(_JobIn), C.POINTER(_JobOut)]
+    L.bt_job_out_free.argtypes = [C.POINTER(_JobOut), C.c_size_t]
+    L.bt_job_out_free.restype = None
+    L.bt_load_synthetic.argtypes = [P, C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    L.bt_load_ohlc.argtypes = [P, C.c_int32, P, P, P, P, P, P]
+    for f in ("bt_run", "bt_sync", "bt_reset_timing"):
+        getattr(L, f).argtypes = [P]
+    L.bt_read_summaries.argtypes = [P, P, C.c_size_t]
+    L.bt_read_sums.argtypes = [P, P, C.c_size_t]
+    L.bt_read_trades.argtypes = [P, P, C.c_size_t]
+    L.bt_read_topk.argtypes = [P, P, C.c_int32]
+    L.bt_read_stats.argtypes = [P, C.POINTER(_Stats)]
+    L.bt_read_close.argtypes = [P, C.c_int32, P, C.c_int32]
+    L.bt_kernel_timing.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                   C.POINTER(C.c_char_p)]
+    L.bt_merge_topk.argtypes = [P, C.c_size_t, C.c_int32, P]
+    L.bt_i128_to_double.argtypes = [C.c_uint64, C.c_int64]
+    L.bt_i128_to_double.restype = C.c_double
+    L.bt_parse_csv.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, P, P, P, C.c_char_p,
+                               C.c_size_t]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        raise BtError(lib().bt_last_error().decode())
+    return rc
+
+
+def _arr(v) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(v, dtype=np.int32))
+
+
+@dataclass
+class Grid:
+    """Worker-side parameter grid (the proto carries none: SURVEY.md §7 hard part 5)."""
+    strategy: int
+    axes: Sequence[Sequence[int]]
+    band_bps: int = 20
+    k_den: int = 2
+    annualization: int = 252
+    _keep: list = field(default_factory=list, repr=False)
+
+    @property
+    def n_params(self) -> int:
+        n = 1
+        for a in self.axes:
+            n *= len(a)
+        return n
+
+    @staticmethod
+    def sma(fast, slow, annualization=252):
+        return Grid(BT_SMA_CROSS, [list(fast), list(slow)], annualization=annualization)
+
+    @staticmethod
+    def ema_ols(span, ols, band_bps=20, annualization=98280):
+        return Grid(BT_EMA_OLS, [list(span), list(ols)], band_bps=band_bps,
+                    annualization=annualization)
+
+    @staticmethod
+    def boll(win, k_num, sl_bps, tp_bps, k_den=2, annualization=98280):
+        return Grid(BT_BOLL, [list(win), list(k_num), list(sl_bps), list(tp_bps)], k_den=k_den,
+                    annualization=annualization)
+
+    def param(self, p: int) -> dict:
+        """Decode a param index (include/bt.h ordering) into named values."""
+        if self.strategy == BT_SMA_CROSS:
+            return {"f": self.axes[0][p // len(self.axes[1])], "s": self.axes[1][p % len(self.axes[1])]}
+        if self.strategy == BT_EMA_OLS:
+            return {"n": self.axes[0][p // len(self.axes[1])], "w": self.axes[1][p % len(self.axes[1])],
+                    "band_bps": self.band_bps}
+        nk, nsl, ntp = (len(a) for a in self.axes[1:])
+        return {"w": self.axes[0][p // (ntp * nsl * nk)], "k_num": self.axes[1][(p // (ntp * nsl)) % nk],
+                "k_den": self.k_den, "sl": self.axes[2][(p // ntp) % nsl], "tp": self.axes[3][p % ntp]}
+
+    def to_c(self, device=0, topk=0, flags=0, host_threads=0, trade_cap=0, stream=None) -> _Config:
+        cfg = _Config()
+        cfg.strategy = self.strategy
+        arrs = [_arr(a) for a in self.axes]
+        self._keep = arrs
+        ptr = [a.ctypes.data_as(C.POINTER(C.c_int32)) for a in arrs]
+        if self.strategy == BT_SMA_CROSS:
+            cfg.n_fast, cfg.n_slow = len(arrs[0]), len(arrs[1])
+            cfg.fast, cfg.slow = ptr
+        elif self.strategy == BT_EMA_OLS:
+            cfg.n_span, cfg.n_ols = len(arrs[0]), len(arrs[1])
+            cfg.span, cfg.ols = ptr
+            cfg.band_bps = self.band_bps
+        else:
+            cfg.n_bwin, cfg.n_k, cfg.n_sl, cfg.n_tp = (len(a) for a in arrs)
+            cfg.bwin, cfg.k_num, cfg.sl_bps, cfg.tp_bps = ptr
+            cfg.k_den = self.k_den
+        cfg.annualization = self.annualization
+        cfg.device, cfg.topk, cfg.flags = device, topk, flags
+        cfg.host_threads, cfg.trade_cap = host_threads, trade_cap
+        cfg.stream = stream
+        return cfg
+
+
+# Pinned grids of BASELINE.json configs.
+def config2_grid():
+    return Grid.sma(range(4, 43, 2), range(50, 241, 10), annualization=252)
+
+
+def config3_grid():
+    return Grid.ema_ols([10, 20, 30, 60, 120, 240, 390, 780],
+                        [15, 30, 60, 120, 240, 390, 780, 1560], band_bps=20, annualization=98280)
+
+
+def config4_grid():
+    return Grid.boll([10, 20, 30, 45, 60, 90, 120, 240], [3, 4, 5, 6], [50, 100],
+                     [50, 100, 200, 400], k_den=2, annualization=98280)
+
+
+def config5_grid():
+    # SMA fast 32 x slow 32 on 1-min bars; max fast*slow = 160*6400 < 2^21 (exact keys)
+    return Grid.sma(range(5, 161, 5), range(200, 6401, 200), annualization=98280)
+
+
+class Engine:
+    """One engine per GPU (one process per GPU)."""
+
+    def __init__(self, grid: Grid, device=0, topk=0, parity=False, timing=False,
+                 trade_cap=0, host_threads=0, stream=None):
+        self.grid = grid
+        flags = (BT_FLAG_PARITY if parity else 0) | (BT_FLAG_TIMING if timing else 0)
+        cfg = grid.to_c(device, topk, flags, host_threads, trade_cap, stream)
+        err = C.create_string_buffer(512)
+        h = lib().bt_engine_create(C.byref(cfg), err, 512)
+        if not h:
+            raise BtError(err.value.decode())
+        self._h = h
+        self.n_params = lib().bt_num_params(h)
+        self.trade_cap = trade_cap
+        self.n_symbols = 0
+        self.topk = topk
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bt_engine_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- HBM-resident path
+    def load_synthetic(self, seed, sym_begin, n_sym, n_bars, freq=BT_DAILY):
+        _check(lib().bt_load_synthetic(self._h, seed & ((1 << 64) - 1), sym_begin, n_sym, n_bars, freq))
+        self.n_symbols = n_sym
+
+    def load_ohlc(self, closes, highs=None, lows=None, sym_ids=None):
+        """closes: list of 1-D int arrays (ragged allowed)."""
+        bars = np.array([len(c) for c in closes], np.int32)
+        offs = np.zeros(len(closes), np.int64)
+        if len(closes):
+            offs[1:] = np.cumsum(bars[:-1])
+        cat = lambda xs: np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in xs])) if len(xs) else np.zeros(1, np.int32)
+        c = cat(closes)
+        h = cat(highs) if highs is not None else None
+        lo = cat(lows) if lows is not None else None
+        ids = np.ascontiguousarray(np.arange(len(closes), dtype=np.int64) if sym_ids is None
+                                   else np.asarray(sym_ids, np.int64))
+        ptr = lambda a: None if a is None else a.ctypes.data
+        _check(lib().bt_load_ohlc(self._h, len(closes), ids.ctypes.data, bars.ctypes.data,
+                                  offs.ctypes.data, ptr(h), ptr(lo), c.ctypes.data))
+        self.n_symbols = len(closes)
+
+    def run(self):
+        _check(lib().bt_run(self._h))
+
+    def sync(self):
+        _check(lib().bt_sync(self._h))
+
+    def summaries(self) -> np.ndarray:
+        n = self.n_symbols * self.n_params
+        out = np.zeros(max(n, 1), SUMMARY_DTYPE)
+        _check(lib().bt_read_summaries(self._h, out.ctypes.data, n))
+        return out[:n].reshape(self.n_symbols, self.n_params)
+
+    def sums(self) -> np.ndarray:
+        n = self.n_symbols * self.n_params
+        out = np.zeros(max(n, 1), SUMS_DTYPE)
+        _check(lib().bt_read_sums(self._h, out.ctypes.data, n))
+        return out[:n].reshape(self.n_symbols, self.n_params)
+
+    def trades(self) -> np.ndarray:
+        n = self.n_symbols * self.n_params * self.trade_cap
+        out = np.zeros(max(n, 1), TRADE_DTYPE)
+        _check(lib().bt_read_trades(self._h, out.ctypes.data, n))
+        return out[:n].reshape(self.n_symbols, self.n_params, self.trade_cap)
+
+    def read_topk(self, k=None) -> np.ndarray:
+        k = k or self.topk
+        out = np.zeros(k, TOPK_DTYPE)
+        m = _check(lib().bt_read_topk(self._h, out.ctypes.data, k))
+        return out[:m]
+
+    def stats(self) -> dict:
+        st = _Stats()
+        _check(lib().bt_read_stats(self._h, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in _Stats._fields_}
+
+    def close_column(self, sym_index, n) -> np.ndarray:
+        out = np.zeros(n, np.int32)
+        _check(lib().bt_read_close(self._h, sym_index, out.ctypes.data, n))
+        return out
+
+    def kernel_timing(self):
+        ms, n, name = C.c_double(), C.c_int64(), C.c_char_p()
+        _check(lib().bt_kernel_timing(self._h, C.byref(ms), C.byref(n), C.byref(name)))
+        return ms.value, n.value, name.value.decode()
+
+    def reset_timing(self):
+        _check(lib().bt_reset_timing(self._h))
+
+    # ---- the JobsReply batch (drop-in for process_incoming_job)
+    def run_batch(self, jobs: Sequence[tuple]) -> list:
+        """jobs: [(id: str, file: bytes)] -> [(status, data: str)] in job order."""
+        n = len(jobs)
+        jin = (_JobIn * max(n, 1))()
+        keep = []
+        for i, (jid, data) in enumerate(jobs):
+            b = bytes(data)
+            idb = jid.encode() if isinstance(jid, str) else bytes(jid)
+            keep += [b, idb]
+            jin[i].id = idb
+            jin[i].file = C.cast(C.c_char_p(b), C.c_void_p)
+            jin[i].len = len(b)
+        jout = (_JobOut * max(n, 1))()
+        _check(lib().bt_run_batch(self._h, n, jin, jout))
+        try:
+            res = [(jout[i].status, C.string_at(jout[i].data, jout[i].len).decode()) for i in range(n)]
+        finally:
+            lib().bt_job_out_free(jout, n)
+        return res
+
+
+def merge_topk(records: np.ndarray, k: int) -> np.ndarray:
+    """Host merge of shard top-k lists (same order as the device: sharpe desc, sym, param)."""
+    recs = np.ascontiguousarray(records, TOPK_DTYPE)
+    out = np.zeros(max(k, 1), TOPK_DTYPE)
+    m = _check(lib().bt_merge_topk(recs.ctypes.data if len(recs) else None, len(recs), k,
+                                   out.ctypes.data))
+    return out[:m]
+
+
+def i128_to_double(lo: int, hi: int) -> float:
+    return lib().bt_i128_to_double(lo & ((1 << 64) - 1), hi)
+
+
+def parse_csv(data: bytes, cap=1 << 22):
+    cap = int(cap)
+    h, lo, c = (np.empty(cap, np.int32) for _ in range(3))
+    err = C.create_string_buffer(256)
+    n = lib().bt_parse_csv(data, len(data), cap, h.ctypes.data, lo.ctypes.data, c.ctypes.data,
+                           err, 256)
+    if n < 0:
+        raise ValueError(err.value.decode())
+    return h[:n].copy(), lo[:n].copy(), c[:n].copy()

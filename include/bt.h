@@ -1,0 +1,170 @@
+/*
+ * bt.h — C ABI of the MI355X-native backtest engine (libbt.so).
+ *
+ * This is the drop-in boundary for the reference worker's job function
+ *     pub fn process_incoming_job(jobs_reply: JobsReply, complete_send: Sender<String>)
+ *     (/root/reference/src/worker/process.rs:13-29)
+ * which today sleeps 1000 ms per job (process.rs:23) and sends `job.id` per job (process.rs:24),
+ * called from the worker's single compute OS thread (/root/reference/src/worker/main.rs:38-42).
+ * The proto contract stays byte-identical (/root/reference/proto/backtesting.proto):
+ * `Job{string id; bytes File}` in (proto:13-16), `CompleteRequest{string id; string data}` out
+ * (proto:29-32). The Rust-side `extern "C"` block a maintainer would add is in INTEGRATION.md.
+ *
+ * Plain C types only. No C++ exception and no abort crosses this boundary: every entry point
+ * catches and returns an int status (0 = OK, < 0 = error; message via bt_last_error()).
+ * The engine is not thread-safe (the reference has exactly one caller thread, main.rs:38-42);
+ * it sets its HIP device on every call, so it may be called from any one OS thread.
+ * Semantics of every number produced: docs/oracle_spec.md.
+ */
+#ifndef BT_H
+#define BT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BT_ABI_VERSION 1
+
+typedef struct bt_engine bt_engine;
+
+enum bt_strategy { BT_SMA_CROSS = 1, BT_EMA_OLS = 2, BT_BOLL = 3 };
+
+enum bt_flags {
+    BT_FLAG_PARITY = 1,  /* also record full trade lists and the int128 return sums */
+    BT_FLAG_TIMING = 2,  /* time the dominant kernel with HIP events (bt_kernel_timing) */
+};
+
+enum bt_freq { BT_DAILY = 0, BT_MINUTE = 1 };
+
+/* Engine configuration. The proto carries no strategy or params (proto:13-16), so the grid is
+ * worker-side configuration (SURVEY.md §7 hard part 5). Arrays are copied at create time. */
+typedef struct bt_config {
+    int32_t strategy;                 /* enum bt_strategy */
+    /* SMA crossover: params = n_fast x n_slow, param = i_fast * n_slow + i_slow */
+    int32_t n_fast, n_slow;
+    const int32_t* fast;
+    const int32_t* slow;
+    /* EMA + rolling OLS: params = n_span x n_ols, param = i_span * n_ols + i_ols */
+    int32_t n_span, n_ols;
+    const int32_t* span;
+    const int32_t* ols;
+    int32_t band_bps;
+    /* Bollinger + SL/TP: param = ((i_w * n_k + i_k) * n_sl + i_sl) * n_tp + i_tp */
+    int32_t n_bwin, n_k, n_sl, n_tp;
+    const int32_t* bwin;
+    const int32_t* k_num;
+    int32_t k_den;
+    const int32_t* sl_bps;
+    const int32_t* tp_bps;
+    int64_t annualization;            /* A in the Sharpe formula: 252 daily, 98280 1-min */
+    int32_t device;                   /* HIP device ordinal */
+    int32_t topk;                     /* k of bt_read_topk (0 = top-k disabled) */
+    int32_t flags;                    /* enum bt_flags */
+    int32_t host_threads;             /* CSV parse threads in bt_run_batch (0 = auto) */
+    int32_t trade_cap;                /* parity mode: trades kept per (symbol, param) */
+    void* stream;                     /* optional hipStream_t to launch on (NULL = own stream) */
+} bt_config;
+
+/* One Job of a JobsReply (proto:13-16). Borrowed for the duration of the call. */
+typedef struct bt_job_in {
+    const char* id;                   /* Job.id (UUIDv4 string from server/main.rs:169) */
+    const uint8_t* file;              /* Job.File bytes (whole CSV, server/main.rs:170) */
+    size_t len;
+} bt_job_in;
+
+/* One CompleteRequest.data (proto:31, UTF-8). Owned by the library: free with bt_job_out_free. */
+typedef struct bt_job_out {
+    char* data;
+    size_t len;
+    int32_t status;                   /* 0 = OK, < 0 = this job failed (data holds {"error":..}) */
+    int32_t n_bars;
+} bt_job_out;
+
+/* Per (symbol, param) result, 48 bytes. */
+typedef struct bt_summary {
+    int32_t n_trades;
+    int32_t status;
+    int64_t pnl;                      /* ticks */
+    int64_t mdd;                      /* ticks */
+    int64_t exposure;                 /* bars held */
+    double sharpe;
+    uint64_t hash;                    /* FNV-1a trade-sequence hash (spec §4) */
+} bt_summary;
+
+typedef struct bt_trade {
+    int32_t entry_bar, exit_bar, side, pad;
+    int64_t entry_px, exit_px;
+} bt_trade;
+
+/* S1, S2 of spec §4 (int128 as lo/hi words); parity mode only. */
+typedef struct bt_sums {
+    uint64_t s1_lo;
+    int64_t s1_hi;
+    uint64_t s2_lo;
+    int64_t s2_hi;
+} bt_sums;
+
+/* Global top-k record (24 B): ordered by sharpe desc, then sym asc, then param asc. */
+typedef struct bt_topk_rec {
+    double sharpe;
+    int32_t sym;
+    int32_t param;
+    int64_t pnl;
+} bt_topk_rec;
+
+typedef struct bt_stats {
+    int64_t n_symbols;
+    int64_t n_params;
+    int64_t bar_evals;                /* sum over symbols of bars x params */
+    int64_t trades;                   /* sum of n_trades over every (symbol, param) */
+    int64_t errors;                   /* symbols rejected */
+} bt_stats;
+
+/* ---- lifecycle */
+bt_engine* bt_engine_create(const bt_config* cfg, char* err, size_t errlen);
+void bt_engine_destroy(bt_engine* e);
+const char* bt_last_error(void);      /* thread-local message of the last failed call */
+int32_t bt_abi_version(void);
+int32_t bt_num_params(const bt_engine* e);
+
+/* ---- drop-in for process_incoming_job: a whole JobsReply in one GPU launch.
+ * outs[i] answers jobs[i] (same order the reference sends completions, process.rs:21-25). */
+int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* outs);
+void bt_job_out_free(bt_job_out* outs, size_t n);
+
+/* ---- HBM-resident path (configs 2-5, bench, multi-GPU shards) */
+/* Generate n_sym synthetic symbols (spec §1) with ids sym_begin.. directly in HBM. */
+int32_t bt_load_synthetic(bt_engine* e, uint64_t seed, int64_t sym_begin, int32_t n_sym,
+                          int32_t n_bars, int32_t freq);
+/* Upload host SoA bars: symbol s has bars[s] rows starting at row offset row_off[s] in h/l/c.
+ * h and l may be NULL unless the strategy is BT_BOLL. */
+int32_t bt_load_ohlc(bt_engine* e, int32_t n_sym, const int64_t* sym_ids, const int32_t* bars,
+                     const int64_t* row_off, const int32_t* h, const int32_t* l,
+                     const int32_t* c);
+int32_t bt_run(bt_engine* e);         /* enqueue the whole hot path on the engine stream */
+int32_t bt_sync(bt_engine* e);
+int32_t bt_read_summaries(bt_engine* e, bt_summary* out, size_t n);     /* n = symbols x params */
+int32_t bt_read_sums(bt_engine* e, bt_sums* out, size_t n);             /* parity mode */
+int32_t bt_read_trades(bt_engine* e, bt_trade* out, size_t n);          /* n = sym x param x cap */
+int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k);        /* returns count */
+int32_t bt_read_stats(bt_engine* e, bt_stats* out);
+/* Read back the synthetic/uploaded close column of one symbol (tests). */
+int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n);
+/* Average device time of the dominant kernel (BT_FLAG_TIMING), and how many launches. */
+int32_t bt_kernel_timing(bt_engine* e, double* total_ms, int64_t* launches, const char** name);
+int32_t bt_reset_timing(bt_engine* e);
+
+/* ---- top-k merge (host): merge sorted record lists from several shards (RCCL gather). */
+int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* out);
+
+/* ---- self-test hooks (host-side helpers the tests call without a GPU) */
+double bt_i128_to_double(uint64_t lo, int64_t hi);
+int32_t bt_parse_csv(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
+                     int32_t* c, char* err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,43 @@
+"""Shared test helpers: oracle-vs-engine comparison (tests only)."""
+import numpy as np
+
+import orc_ffi as F
+
+
+def oracle_row(strategy, grid, ohlc, ann, cap=0):
+    """Run the C oracle for every param of `grid` on one symbol; returns (summaries, trades)."""
+    o, h, lo, c = ohlc
+    out, trades = [], []
+    for p in range(grid.n_params):
+        kw = grid.param(p)
+        if strategy == "sma":
+            s, tr = F.sma(c, kw["f"], kw["s"], ann, cap)
+        elif strategy == "ema_ols":
+            s, tr = F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], ann, cap)
+        else:
+            s, tr = F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], ann, cap)
+        out.append(s)
+        trades.append(tr)
+    return out, trades
+
+
+FIELDS = ("n_trades", "pnl", "mdd", "exposure", "hash")
+
+
+def compare_summary(gpu, orc, where=""):
+    """Bit-exact comparison of one engine summary vs one oracle summary."""
+    for f in FIELDS:
+        assert int(gpu[f]) == int(orc[f]), f"{where}: {f} gpu={gpu[f]} oracle={orc[f]}"
+    # Sharpe: bit-exact by construction (exact int128 sums, fixed op sequence); the north_star
+    # tolerance (1e-9 relative) is asserted as well so a failure message shows the size.
+    g, o = float(gpu["sharpe"]), float(orc["sharpe"])
+    assert abs(g - o) <= 1e-9 * max(abs(o), 1e-300), f"{where}: sharpe {g!r} vs {o!r}"
+    assert g == o, f"{where}: sharpe not bit-exact {g!r} vs {o!r}"
+
+
+def compare_trades(gpu_tr, orc_tr, n, where=""):
+    got = [tuple(int(x) for x in (t["entry_bar"], t["exit_bar"], t["side"], t["entry_px"], t["exit_px"]))
+           for t in gpu_tr[:n]]
+    exp = [tuple(int(x) for x in (t["entry_bar"], t["exit_bar"], t["side"], t["entry_px"], t["exit_px"]))
+           for t in orc_tr[:n]]
+    assert got == exp, f"{where}: trade lists differ (first diff at {next((i for i,(a,b) in enumerate(zip(got,exp)) if a!=b), None)})"

@@ -1,0 +1,108 @@
+"""CPU-side checks of the C ABI (include/bt.h): the library loads, exports every declared
+symbol, its host helpers are right, and it fails loudly (no CPU fallback) without a GPU."""
+import ctypes as C
+import json
+import os
+import random
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from dbx_amd import engine as E
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    text = open(os.path.join(ROOT, "include", "bt.h")).read()
+    return sorted(set(re.findall(r"\b(bt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(E.LIB_PATH)
+    names = _declared_symbols()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", E.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (bt_[a-z0-9_]+)$", out, re.M))
+    assert set(names) <= exported
+
+
+def test_library_targets_gfx950_only():
+    blob = open(E.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}
+
+
+def test_abi_version_and_no_gpu_failure():
+    assert D.lib().bt_abi_version() == 1
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present")
+    with pytest.raises(D.BtError, match="device|HIP"):
+        D.Engine(D.config2_grid())
+
+
+def test_config_validation():
+    # exact-key range of the SMA kernel: max fast * max slow must stay < 2^21
+    with pytest.raises(D.BtError, match="exact-key"):
+        D.Engine(D.Grid.sma([3000], [1000]))
+    with pytest.raises(D.BtError, match="empty axis"):
+        D.Engine(D.Grid.sma([], [10]))
+    with pytest.raises(D.BtError, match="annualization"):
+        D.Engine(D.Grid.sma([2], [10], annualization=0))
+
+
+def test_i128_to_double_round_to_nearest_even():
+    rng = random.Random(5)
+    cases = [0, 1, -1, 2**53, 2**53 + 1, 2**53 + 3, -(2**53 + 1), 2**64 - 1, 2**100 + 2**47,
+             2**100 + 2**47 + 1, -(2**127), 2**127 - 1, 3 << 70]
+    cases += [rng.getrandbits(rng.randint(1, 126)) * rng.choice([1, -1]) for _ in range(2000)]
+    for x in cases:
+        lo, hi = x & (2**64 - 1), x >> 64
+        assert E.i128_to_double(lo, hi) == float(x), x
+
+
+def test_product_csv_parser_matches_golden(golden_dir):
+    g = json.load(open(os.path.join(golden_dir, "csv.json")))
+    for key in ("daily", "minute"):
+        h, lo, c = E.parse_csv(g[key]["text"].encode())
+        assert c.tolist() == g[key]["c"] and h.tolist() == g[key]["h"] and lo.tolist() == g[key]["l"]
+    for name, case in g["good"].items():
+        h, lo, c = E.parse_csv(case["text"].encode())
+        assert c.tolist() == case["c"], name
+    for name, text in g["bad"].items():
+        with pytest.raises(ValueError):
+            E.parse_csv(text.encode())
+
+
+def test_product_csv_parser_matches_oracle_on_synthetic_files():
+    import oracle_np as N
+    import orc_ffi as F
+    for sym, bars, freq in [(0, 300, 0), (5, 1000, 1)]:
+        o, h, lo, c, v = N.gen(9, [sym], bars, freq)
+        text = N.csv_bytes(o[0], h[0], lo[0], c[0], v[0], freq)
+        ph, pl, pc = E.parse_csv(text)
+        fo, fh, fl, fc, fv = F.parse_csv(text)
+        assert np.array_equal(ph, fh) and np.array_equal(pl, fl) and np.array_equal(pc, fc)
+
+
+def test_merge_topk_order():
+    rng = np.random.default_rng(0)
+    recs = np.zeros(500, D.TOPK_DTYPE)
+    recs["sharpe"] = rng.choice([0.5, 1.0, -2.0, 3.25], 500)
+    recs["sym"] = rng.integers(0, 50, 500)
+    recs["param"] = rng.integers(0, 400, 500)
+    got = D.merge_topk(recs, 40)
+    exp = sorted(recs.tolist(), key=lambda r: (-r[0], r[1], r[2]))[:40]
+    assert [tuple(r) for r in got.tolist()] == [tuple(r) for r in exp]
+    assert len(D.merge_topk(recs[:0], 5)) == 0

@@ -1,0 +1,174 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the C oracle, bit-exact.
+
+North_star bar: trade counts and entry/exit bars bit-exact; PnL/Sharpe/MDD within 1e-9
+relative in fp64 (here every field is bit-exact, Sharpe included — see docs/oracle_spec.md §3).
+"""
+import numpy as np
+import pytest
+
+import dbx_amd as D
+import orc_ffi as F
+from helpers import compare_summary, compare_trades, oracle_row
+
+pytestmark = pytest.mark.gpu
+
+CAP = 4096
+
+
+def _gen(seed, syms, bars, freq):
+    cols = [F.gen(seed, s, bars, freq) for s in syms]
+    o = [c[0] for c in cols]
+    h = [c[1] for c in cols]
+    lo = [c[2] for c in cols]
+    c = [c[3] for c in cols]
+    return o, h, lo, c
+
+
+def test_synthetic_generator_matches_oracle():
+    g = D.config2_grid()
+    with D.Engine(g) as e:
+        e.load_synthetic(0x5EED, 4990, 10, 2520, D.BT_DAILY)
+        for i in (0, 3, 9):
+            got = e.close_column(i, 2520)
+            exp = F.gen(0x5EED, 4990 + i, 2520, 0)[3]
+            assert np.array_equal(got, exp)
+    with D.Engine(D.config4_grid()) as e:  # minute bars, high/low columns generated too
+        e.load_synthetic(7, 3, 2, 5000, D.BT_MINUTE)
+        assert np.array_equal(e.close_column(1, 5000), F.gen(7, 4, 5000, 1)[3])
+
+
+@pytest.mark.parametrize("bars", [700, 64, 65, 1, 2, 130])
+def test_sma_parity_synthetic(bars):
+    grid = D.Grid.sma([2, 4, 6, 10, 42], [3, 50, 120, 240, 600], annualization=252)
+    syms = list(range(5))
+    o, h, lo, c = _gen(0x5EED, syms, bars, 0)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 0, len(syms), bars, D.BT_DAILY)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in syms:
+        orc, otr = oracle_row("sma", grid, (o[s], h[s], lo[s], c[s]), 252, CAP)
+        for p in range(grid.n_params):
+            where = f"sym {s} param {grid.param(p)} bars {bars}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_sma_parity_ragged_and_edges(golden_dir):
+    import json, os
+    edge = json.load(open(os.path.join(golden_dir, "edge.json")))
+    closes = [np.array(x["c"], np.int32) for x in edge]
+    grid = D.Grid.sma([2, 3, 4], [3, 5, 50], annualization=252)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_ohlc(closes)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("sma", grid, (cl, cl, cl, cl), 252, CAP)
+        for p in range(grid.n_params):
+            where = f"{edge[s]['name']} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_sma_sums_exact():
+    grid = D.Grid.sma([4, 10], [50, 60], annualization=252)
+    o, h, lo, c = _gen(11, [0, 1], 900, 0)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(11, 0, 2, 900, D.BT_DAILY)
+        e.run()
+        sums = e.sums()
+    for s in range(2):
+        orc, _ = oracle_row("sma", grid, (o[s], h[s], lo[s], c[s]), 252)
+        for p in range(grid.n_params):
+            assert F.i128(sums[s, p]["s1_lo"], sums[s, p]["s1_hi"]) == F.i128(orc[p]["s1_lo"], orc[p]["s1_hi"])
+            assert F.i128(sums[s, p]["s2_lo"], sums[s, p]["s2_hi"]) == F.i128(orc[p]["s2_lo"], orc[p]["s2_hi"])
+
+
+@pytest.mark.parametrize("strategy", ["ema_ols", "boll"])
+def test_lane_strategies_parity(strategy):
+    if strategy == "ema_ols":
+        grid = D.Grid.ema_ols([3, 10, 60, 390], [4, 15, 120, 780], band_bps=20)
+    else:
+        grid = D.Grid.boll([3, 10, 45, 240], [1, 3, 6], [50, 100], [50, 400], k_den=2)
+    bars = 3000
+    o, h, lo, c = _gen(0x5EED, [0, 1, 2], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 0, 3, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(3):
+        orc, otr = oracle_row(strategy, grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_topk_exact_order():
+    grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
+    S, bars, k = 40, 800, 25
+    with D.Engine(grid, topk=k) as e:
+        e.load_synthetic(3, 100, S, bars, D.BT_DAILY)
+        e.run()
+        top = e.read_topk()
+        allr = e.summaries()
+    recs = [(-float(allr[s, p]["sharpe"]), 100 + s, p) for s in range(S) for p in range(grid.n_params)]
+    recs.sort()
+    exp = [(r[1], r[2]) for r in recs[:k]]
+    assert [(int(t["sym"]), int(t["param"])) for t in top] == exp
+    assert all(float(top[i]["sharpe"]) >= float(top[i + 1]["sharpe"]) for i in range(k - 1))
+
+
+def test_run_batch_csv_jobs():
+    import oracle_np as N
+    grid = D.Grid.sma([4, 10], [50, 120], annualization=252)
+    jobs, series = [], []
+    for s, bars in [(0, 300), (1, 451), (2, 64)]:
+        o, h, lo, c, v = N.gen(0x5EED, [s], bars, 0)
+        jobs.append((f"job-{s}", N.csv_bytes(o[0], h[0], lo[0], c[0], v[0], 0)))
+        series.append(c[0].astype(np.int32))
+    jobs.insert(1, ("bad", b"2010-01-04,1,2,1\n"))
+    with D.Engine(grid) as e:
+        res = e.run_batch(jobs)
+    assert res[1][0] < 0 and '"error"' in res[1][1]
+    good = [r for i, r in enumerate(res) if i != 1]
+    for (status, data), cl in zip(good, series):
+        assert status == 0
+        lines = data.strip().split("\n")
+        assert len(lines) == grid.n_params
+        orc, _ = oracle_row("sma", grid, (cl, cl, cl, cl), 252)
+        import json
+        for p, line in enumerate(lines):
+            j = json.loads(line)
+            assert j["param"] == p and j["n"] == int(orc[p]["n_trades"])
+            assert j["pnl"] == int(orc[p]["pnl"]) and j["mdd"] == int(orc[p]["mdd"])
+            assert float(j["sharpe"]) == float(orc[p]["sharpe"])
+            assert int(j["h"], 16) == int(orc[p]["hash"])
+
+
+def test_config2_full_shape_sampled_parity():
+    """BASELINE config 2 at full size on the GPU; 48 sampled symbols checked against the
+    multithreaded C oracle, plus size-independent properties over all 2M lanes."""
+    grid = D.config2_grid()
+    S, bars = 5000, 2520
+    with D.Engine(grid, topk=100) as e:
+        e.load_synthetic(0x5EED, 0, S, bars, D.BT_DAILY)
+        e.run()
+        allr = e.summaries()
+        st = e.stats()
+        top = e.read_topk()
+    assert st["bar_evals"] == S * bars * grid.n_params
+    assert st["trades"] == int(allr["n_trades"].sum())
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(S, 48, replace=False))
+    closes = np.stack([F.gen(0x5EED, int(s), bars, 0)[3] for s in sample])
+    orc = F.sma_grid_mt(closes, np.arange(4, 43, 2), np.arange(50, 241, 10), 252, 8)
+    for i, s in enumerate(sample):
+        for p in range(grid.n_params):
+            compare_summary(allr[s, p], orc[i, p], f"config2 sym {s} param {p}")
+    flat = allr.reshape(-1)
+    order = np.lexsort((np.tile(np.arange(grid.n_params), S), np.repeat(np.arange(S), grid.n_params),
+                        -flat["sharpe"]))
+    exp = [(int(i // grid.n_params), int(i % grid.n_params)) for i in order[:100]]
+    assert [(int(t["sym"]), int(t["param"])) for t in top] == exp
