@@ -1,0 +1,145 @@
+"""Dispatcher counterpart of the reference server (`src/server/main.rs`), for driving the
+worker end-to-end (BASELINE config 1) without Rust or protoc. SURVEY.md §8(f) row 3.
+
+Mirrored semantics:
+  * Dispatcher{files, peers, jobs_completed}                               main.rs:26-34
+  * peer-health thread: every 100 ms drop peers silent for > 10 s          main.rs:39-52, 183-190
+  * complete_job records id -> True (and, new here, keeps `data`)          main.rs:66-78
+  * send_status updates an existing peer's status only                     main.rs:80-102
+  * request_jobs upserts the peer, splits off jobs, reads each file whole,
+    assigns a UUIDv4 id, drops unreadable paths                            main.rs:105-147,164-180
+  * split_off_n_jobs: None on empty; drain all if n >= len; otherwise
+    Vec::split_off(n) — hand out the TAIL [n, len) and keep the first n    main.rs:151-162
+  * empty queue: Status::new(Code::Ok, "No more jobs available")           main.rs:139-141
+  * replies gzip-compressed                                                main.rs:212
+Known reference quirk kept visible, not copied: peers are keyed by the server's own
+local_addr (main.rs:84,109); here they are keyed by the client's peer string.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import threading
+import time
+import uuid
+from concurrent import futures
+from typing import Dict, List, Optional
+
+import grpc
+
+from . import proto as P
+
+log = logging.getLogger("dbx_amd.dispatcher")
+
+
+def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
+    """main.rs:151-162, including Vec::split_off's tail semantics."""
+    if not files:
+        return None
+    if n >= len(files):
+        out = files[:]
+        files.clear()
+        return out
+    n = max(n, 0)
+    tail = files[n:]
+    del files[n:]
+    return tail
+
+
+class Dispatcher:
+    def __init__(self, paths: List[str], prune_after_s: float = 10.0, check_every_s: float = 0.1):
+        self.files = list(paths)
+        self.files_lock = threading.Lock()
+        self.peers: Dict[str, dict] = {}
+        self.peers_lock = threading.Lock()
+        self.jobs_completed: Dict[str, bool] = {}
+        self.results: Dict[str, str] = {}      # results sink (the reference ignores data)
+        self.job_paths: Dict[str, str] = {}
+        self.done_lock = threading.Lock()
+        self._stop = threading.Event()
+        self.prune_after_s = prune_after_s
+        threading.Thread(target=self._health, args=(check_every_s,), daemon=True).start()
+
+    def _health(self, every):
+        while not self._stop.is_set():
+            now = time.time()
+            with self.peers_lock:
+                for addr, peer in list(self.peers.items()):
+                    if now - peer["last_connection"] > self.prune_after_s:
+                        log.info("Removing addr %s", addr)
+                        del self.peers[addr]
+            time.sleep(every)
+
+    def close(self):
+        self._stop.set()
+
+    # ---- RPC handlers
+    def complete_job(self, req, ctx):
+        with self.done_lock:
+            self.jobs_completed[req.id] = True
+            self.results[req.id] = req.data
+        return P.CompleteReply()
+
+    def send_status(self, req, ctx):
+        with self.peers_lock:
+            peer = self.peers.get(ctx.peer())
+            if peer is not None:
+                peer["status"] = req.status
+        return P.StatusReply()
+
+    def request_jobs(self, req, ctx):
+        with self.peers_lock:
+            self.peers[ctx.peer()] = {"status": P.IDLE, "last_connection": time.time()}
+        with self.files_lock:
+            files = split_off_n_jobs(self.files, req.cores)
+        if files is None:
+            ctx.abort(grpc.StatusCode.NOT_FOUND, "No more jobs available")
+        jobs = []
+        for path in files:
+            jid = str(uuid.uuid4())
+            try:
+                with open(path, "rb") as f:
+                    data = f.read()
+            except OSError:
+                continue
+            self.job_paths[jid] = path
+            jobs.append(P.Job(id=jid, File=data))
+        log.info("Num files to run: %d", len(jobs))
+        return P.JobsReply(jobs=jobs)
+
+
+def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20):
+    ser = lambda m: m.SerializeToString()  # noqa: E731
+    handlers = {
+        "CompleteJob": grpc.unary_unary_rpc_method_handler(
+            dispatcher.complete_job, request_deserializer=P.CompleteRequest.FromString,
+            response_serializer=ser),
+        "SendStatus": grpc.unary_unary_rpc_method_handler(
+            dispatcher.send_status, request_deserializer=P.StatusRequest.FromString,
+            response_serializer=ser),
+        "RequestJobs": grpc.unary_unary_rpc_method_handler(
+            dispatcher.request_jobs, request_deserializer=P.JobsRequest.FromString,
+            response_serializer=ser),
+    }
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=8),
+                         compression=grpc.Compression.Gzip,
+                         options=[("grpc.max_send_message_length", max_send)])
+    server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(P.SERVICE, handlers),))
+    port = server.add_insecure_port(addr)
+    server.start()
+    return server, port
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="backtest job dispatcher")
+    ap.add_argument("paths", nargs="+")
+    ap.add_argument("--addr", default="[::1]:50051")  # main.rs:195
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    d = Dispatcher(a.paths)
+    server, _ = serve(d, a.addr)
+    server.wait_for_termination()
+
+
+if __name__ == "__main__":
+    main()

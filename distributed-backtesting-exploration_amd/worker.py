@@ -1,0 +1,157 @@
+"""Worker counterpart of the reference (`src/worker/*.rs`) with the HIP engine as its job path.
+
+Reference behaviour mirrored (control plane unchanged; only the job function is new):
+  * one compute OS thread fed by a bounded(1024) channel            main.rs:32-42
+  * a 250 ms job tick: SendStatus(IDLE) then RequestJobs(cores)      main.rs:68,76-78; handlers.rs:34-64
+  * a 1 s status tick: SendStatus(RUNNING) only while PROC_FLAG      main.rs:69,73-75; handlers.rs:14-32
+  * completions forwarded as CompleteRequest{id, data}               main.rs:80-83
+  * process_incoming_job sets PROC_FLAG, handles the jobs of one
+    JobsReply in order, sends one completion per job, clears it      process.rs:13-29
+The only change is inside process_incoming_job: instead of `sleep(1000 ms)` per job
+(process.rs:23) the whole JobsReply is one batch call into libbt.so (bt_run_batch), and the
+completion carries the results string as `data` (the reference sends `data = id`, main.rs:82).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import queue
+import threading
+import time
+from typing import Callable, Optional, Sequence
+
+import grpc
+
+from . import proto as P
+
+log = logging.getLogger("dbx_amd.worker")
+
+# process.rs / main.rs statics
+PROC_FLAG = threading.Event()   # main.rs:24 (OnceLock<AtomicBool>)
+CONNECTED = threading.Event()   # main.rs:25
+
+# A processor maps [(id, file_bytes)] -> [data_string] (same order). The product processor is
+# the HIP engine (engine_processor); tests may plug the C oracle in as a checker.
+Processor = Callable[[Sequence[tuple]], Sequence[str]]
+
+
+def engine_processor(engine) -> Processor:
+    def run(jobs):
+        return [data for _status, data in engine.run_batch(jobs)]
+    return run
+
+
+def process_incoming_job(jobs_reply, complete_send: "queue.Queue", processor: Processor) -> None:
+    """Drop-in for `process_incoming_job` (process.rs:13-29): PROC_FLAG up, the reply's jobs
+    processed (one GPU batch), one (id, data) completion per job in job order, PROC_FLAG down."""
+    PROC_FLAG.set()
+    try:
+        jobs = [(j.id, j.File) for j in jobs_reply.jobs]
+        if jobs:
+            results = processor(jobs)
+            for (jid, _), data in zip(jobs, results):
+                complete_send.put((jid, data))
+    finally:
+        PROC_FLAG.clear()
+
+
+class Worker:
+    def __init__(self, target: str, processor: Processor, cores: Optional[int] = None,
+                 job_tick: float = 0.250, status_tick: float = 1.0,
+                 max_receive: int = 4 * 1024 * 1024):
+        self.target = target
+        self.processor = processor
+        # handlers.rs:35 reports num_cpus/2; a GPU worker reports its batch capacity instead
+        self.cores = cores if cores is not None else max(1, (os.cpu_count() or 2) // 2)
+        self.job_tick, self.status_tick = job_tick, status_tick
+        self.reply_q: "queue.Queue" = queue.Queue(maxsize=1024)      # main.rs:32
+        self.complete_q: "queue.Queue" = queue.Queue(maxsize=1024)   # main.rs:33
+        self.stop = threading.Event()
+        opts = [("grpc.max_receive_message_length", max_receive)]
+        self.channel = grpc.insecure_channel(target, options=opts)
+        u = self.channel.unary_unary
+        ser = lambda m: m.SerializeToString()  # noqa: E731
+        self._status = u(P.method_path("SendStatus"), request_serializer=ser,
+                         response_deserializer=P.StatusReply.FromString)
+        self._request = u(P.method_path("RequestJobs"), request_serializer=ser,
+                          response_deserializer=P.JobsReply.FromString)
+        self._complete = u(P.method_path("CompleteJob"), request_serializer=ser,
+                           response_deserializer=P.CompleteReply.FromString)
+
+    # main.rs:38-42 — the compute OS thread
+    def _compute(self):
+        while not self.stop.is_set():
+            try:
+                reply = self.reply_q.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            process_incoming_job(reply, self.complete_q, self.processor)
+
+    # handlers.rs:14-32
+    def send_status(self):
+        if PROC_FLAG.is_set():
+            try:
+                self._status(P.StatusRequest(status=P.RUNNING))
+            except grpc.RpcError as why:
+                log.error("%s", why)
+
+    # handlers.rs:34-64
+    def handle_job(self):
+        try:
+            self._status(P.StatusRequest(status=P.IDLE))
+        except grpc.RpcError as why:
+            if CONNECTED.is_set():
+                log.error("Unable to send status: %s", why)
+            CONNECTED.clear()
+        try:
+            reply = self._request(P.JobsRequest(cores=self.cores))
+        except grpc.RpcError:
+            return  # empty queue / server gone: the reference ignores it (handlers.rs:59)
+        self.reply_q.put(reply)
+
+    def run(self, duration: Optional[float] = None):
+        CONNECTED.set()
+        th = threading.Thread(target=self._compute, daemon=True, name="compute")
+        th.start()
+        t_end = None if duration is None else time.monotonic() + duration
+        next_job = next_status = time.monotonic()
+        try:
+            while not self.stop.is_set() and (t_end is None or time.monotonic() < t_end):
+                now = time.monotonic()
+                if now >= next_status:
+                    self.send_status()
+                    next_status = now + self.status_tick
+                if now >= next_job:
+                    self.handle_job()
+                    next_job = now + self.job_tick
+                try:  # main.rs:80-83
+                    jid, data = self.complete_q.get(timeout=0.01)
+                    self._complete(P.CompleteRequest(id=jid, data=data))
+                except queue.Empty:
+                    pass
+        finally:
+            self.stop.set()
+            th.join(timeout=5)
+            self.channel.close()
+
+
+def main(argv=None):
+    from .engine import BT_BOLL, BT_EMA_OLS, Engine, config2_grid, config3_grid, config4_grid
+    ap = argparse.ArgumentParser(description="GPU worker for the backtesting dispatcher")
+    ap.add_argument("--target", default="[::1]:50051")            # main.rs:48
+    ap.add_argument("--strategy", default="sma", choices=["sma", "ema_ols", "boll"])
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--cores", type=int, default=None, help="jobs per RequestJobs")
+    ap.add_argument("--max-receive-mb", type=int, default=4)
+    ap.add_argument("--duration", type=float, default=None)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    grid = {"sma": config2_grid, "ema_ols": config3_grid, "boll": config4_grid}[a.strategy]()
+    eng = Engine(grid, device=a.device)
+    Worker(a.target, engine_processor(eng), a.cores,
+           max_receive=a.max_receive_mb << 20).run(a.duration)
+
+
+if __name__ == "__main__":
+    main()
