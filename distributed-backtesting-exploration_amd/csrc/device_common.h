@@ -20,6 +20,12 @@ struct Agg {
 
 __device__ __forceinline__ Agg agg_one(int32_t x) { return Agg{x, x, 0, 0}; }
 
+// Field-wise select (keeps both operands in registers: a ternary on the struct can become a
+// two-element private array indexed at run time, i.e. scratch memory).
+__device__ __forceinline__ Agg agg_sel(bool c, const Agg& a, const Agg& b) {
+    return Agg{c ? a.mx : b.mx, c ? a.mn : b.mn, c ? a.dd : b.dd, c ? a.du : b.du};
+}
+
 // a happens before b
 __device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) {
     Agg r;
@@ -70,11 +76,21 @@ __device__ __forceinline__ Agg dst_query(const Agg* D, const int32_t* cT, int a,
     return agg_merge(D[L * kTile + a], D[L * kTile + b]);
 }
 
+// Branch-free form: for a == b level 0 holds the single bar (D[0][a] == one(c_a)), and
+// merging it with itself leaves max/min unchanged and gives drawdown/draw-up 0.
+__device__ __forceinline__ Agg dst_query_bf(const Agg* D, int a, int b) {
+    const unsigned x = (unsigned)(a ^ b);
+    const int L = x ? 31 - __builtin_clz(x) : 0;
+    return agg_merge(D[L * kTile + a], D[L * kTile + b]);
+}
+
 // Per-lane trade accounting state (spec §4), updated only at trade events.
+// S1/S2 (spec §4) of an open trade are folded in at the entry (-side*Q1[e], -Q2[e]) and the
+// exit (+side*Q1[x], +Q2[x]), so no per-trade prefix value has to stay live in registers.
 struct Acct {
-    int32_t pos, e, ce, ntr;
-    int64_t R, peak, mdd, expo;
-    i128 s1, s2, q1e, q2e;
+    int32_t pos, e, ce, ntr, expo;
+    int64_t R, peak, mdd;
+    i128 s1, s2;
     uint64_t h;
     Agg agg;  // closes [e, current tile start - 1] while a trade spans tiles
 };
@@ -84,8 +100,9 @@ __device__ __forceinline__ void acct_init(Acct& a) {
     a.e = 0;
     a.ce = 0;
     a.ntr = 0;
-    a.R = a.peak = a.mdd = a.expo = 0;
-    a.s1 = a.s2 = a.q1e = a.q2e = 0;
+    a.expo = 0;
+    a.R = a.peak = a.mdd = 0;
+    a.s1 = a.s2 = 0;
     a.h = kFnvOff;
     a.agg = Agg{0, 0, 0, 0};
 }
@@ -100,15 +117,15 @@ __device__ __forceinline__ void acct_close(Acct& a, int x, int64_t px, const Agg
         emax = a.R + ((int64_t)st.mx - a.ce);
         path = st.dd;
         pnl = px - a.ce;
-        a.s1 += q1x - a.q1e;
+        a.s1 += q1x;
     } else {
         emin = a.R + ((int64_t)a.ce - st.mx);
         emax = a.R + ((int64_t)a.ce - st.mn);
         path = st.du;
         pnl = (int64_t)a.ce - px;
-        a.s1 -= q1x - a.q1e;
+        a.s1 -= q1x;
     }
-    a.s2 += q2x - a.q2e;
+    a.s2 += q2x;
     a.mdd = max(a.mdd, max(a.peak - emin, path));
     a.peak = max(a.peak, emax);
     a.R += pnl;
@@ -134,8 +151,9 @@ __device__ __forceinline__ void acct_open(Acct& a, int t, int side, int32_t ce, 
     a.pos = side;
     a.e = t;
     a.ce = ce;
-    a.q1e = q1;
-    a.q2e = q2;
+    if (side > 0) a.s1 -= q1;
+    else a.s1 += q1;
+    a.s2 -= q2;
 }
 
 __device__ __forceinline__ void acct_write(const Acct& a, int bars, double sqrt_ann, size_t gi,

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -135,10 +136,9 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             e->grid.nb = c.n_slow;
             e->grid.nc = e->grid.nd = 1;
             e->grid.wmax = (int32_t)std::max(mf, ms);
-            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + kTile);
-            const size_t nw = (size_t)c.n_fast + c.n_slow;
-            const size_t lds = (size_t)e->grid.ring * 8 + ((nw * (kTile + 1) * 8 + 15) & ~size_t(15)) +
-                               6 * kTile * 16 + 4 * kTile * 8 + kTile * 4 + nw * 4;
+            // prefix ring: windows + three tiles in flight (k_sma.hip pipeline)
+            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
+            const size_t lds = sma_lds_bytes(e->grid);
             if (lds > 160 * 1024) return "SMA grid needs more LDS than a CU has (windows too long)";
             break;
         }
@@ -422,6 +422,7 @@ bt_engine* bt_engine_create(const bt_config* cfg, char* err, size_t errlen) {
             e->own_stream = true;
         }
         upload_grid(e);
+        if (const char* ab = getenv("BT_ABLATE")) e->grid.ablate = atoi(ab);  // profiling aid
         return e;
     } catch (const HipFail& f) {
         delete e;

@@ -27,6 +27,7 @@ struct Grid {
     int32_t wmax;                  // largest window of the grid (SMA ring sizing)
     int32_t ring;                  // SMA prefix ring length (power of two >= wmax + kTile)
     double sqrt_ann;               // sqrt((double)annualization), computed on the host
+    int32_t ablate;                // profiling only (env BT_ABLATE): phases to skip, 0 = none
     const int32_t* a;              // device arrays
     const int32_t* b;
     const int32_t* c;
@@ -46,6 +47,7 @@ struct Out {
 // Launchers (k_*.hip). All enqueue on `st` and return hipError_t.
 hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
                       int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st);
+size_t sma_lds_bytes(const Grid& g);  // dynamic LDS of the SMA kernel for this grid
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                       const Out& out, bool parity, hipStream_t st);
 // q/q2: [rows] int64 scratch for the fixed-point returns (spec §3) of every bar.

@@ -4,24 +4,167 @@
 // process_incoming_job (/root/reference/src/worker/process.rs:21-25). Spec: docs/oracle_spec.md
 // §3-§5 (SMA). Checked bit-for-bit against oracle/oracle.c::orc_sma.
 //
-// Layout and schedule (per 64-bar tile, all in LDS; HBM is read once: 4 B of close per bar):
-//  1. wave 0 scans the tile's closes: exact prefix sums of close (int64 -> double, exact below
-//     2^53) appended to a ring of the last `ring` prefix values; fixed-point returns q, q2 and
-//     their int128 prefix sums (spec §3).
-//  2. all waves build the tile's disjoint sparse table of the close path (max, min, drawdown,
-//     draw-up) and the SMA keys K[w][b] = RN(window_sum / w) for every window of the grid.
-//     Comparing RN(F/f) with RN(L/s) is exactly the spec's F*s vs L*f test when f*s < 2^21 and
-//     close < 2^31 (distinct rationals differ by >= 1/(f*s) > 1 ulp, equal ones round equal);
-//     the engine rejects grids outside that range. Warm-up keys are NaN (compare false).
-//  3. each lane compares its fast/slow key rows for 64 bars -> two 64-bit words G (fast > slow)
-//     and L (fast < slow). The position path of the whole tile then follows bit-parallel
-//     (a set/reset latch is an add-with-carry: LONG = carries of ~L + G + [pos == +1]),
-//     so the per-bar cost is two compares and two shifts.
-//  4. each lane walks only its position flips (ctz loop): per trade O(1) work — PnL, MTM
-//     drawdown from the sparse table, Sharpe sums as int128 prefix differences, hash.
+// HBM is read once (4 B of close per bar per symbol); everything else lives in LDS, one 64-bar
+// tile at a time, in a three-stage software pipeline with ONE workgroup barrier per tile:
+//   stage 1, tile k+2 (the last wave, "helper"): exact int64 prefix of close appended to a ring
+//            of doubles (exact below 2^53); fixed-point returns q, q2 (spec §3) and their
+//            in-tile int64 prefixes + int128 tile base; the tile's disjoint sparse table (DST) of
+//            the close path (max, min, drawdown, draw-up), built by log-doubling shuffles.
+//   stage 2, tile k+1 (all waves): int32 SMA keys K[w][b] = floor(window_sum / w) for every
+//            window of the grid (one f64 multiply + exact fix-up, no division).
+//   stage 3, tile k (all waves, lane = (fast, slow) pair): 2 integer compares per bar give two
+//            64-bit words G (fast key > slow key) and L (<). Keys are monotone in the exact SMA,
+//            so a strict key order is the exact order; equal keys (rare) are settled exactly
+//            (F*s vs L*f in f64, products < 2^53). The whole tile's position path then follows
+//            bit-parallel: a set/reset latch is an add-with-carry (LONG = carries of
+//            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
+//            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
 #include "device_common.h"
 
 namespace bt {
+
+namespace {
+
+constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned for b128 reads
+constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
+
+struct SmaLds {                       // byte offsets into dynamic LDS
+    size_t ring, keys, invw, win, dst, ct, ql, qb, total;
+};
+
+__host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
+    SmaLds L;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
+    L.ring = take((size_t)ring * 8);
+    L.keys = take((size_t)2 * nw * kKS * 4);
+    L.invw = take((size_t)nw * 8);
+    L.win = take((size_t)nw * 4);
+    L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
+    L.ct = take((size_t)kStages * kTile * 4);
+    L.ql = take((size_t)kStages * 2 * kTile * 8);
+    L.qb = take((size_t)kStages * 4 * 8);
+    L.total = o;
+    return L;
+}
+
+// Wave-wide shuffle of an Agg from lane `src`.
+__device__ __forceinline__ Agg shfl_agg(const Agg& a, int src) {
+    return Agg{__shfl(a.mx, src, 64), __shfl(a.mn, src, 64), __shfl(a.dd, src, 64),
+               __shfl(a.du, src, 64)};
+}
+
+__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Stage 1 for one tile, executed by one whole wave (lane = bar of the tile).
+struct ScanCarry {
+    int64_t P;          // sum of closes before the tile
+    i128 Q1, Q2;        // sum of q, q2 before the tile
+    int32_t prevc;      // close of the bar before the tile
+};
+
+__device__ __forceinline__ void stage_scan(const int32_t* __restrict__ crow, int B, int t0, int lane,
+                                           int R, double* ring, int32_t* cT, int64_t* ql,
+                                           uint64_t* qb, Agg* D, ScanCarry& cy) {
+    const int t = t0 + lane;
+    const bool valid = t < B;
+    const int32_t c = valid ? crow[t] : 0;
+    int32_t cp = __shfl_up(c, 1, 64);
+    if (lane == 0) cp = cy.prevc;
+    const int64_t inc = wave_scan_i64((int64_t)c, lane);
+    ring[(t + 1) & (R - 1)] = (double)(cy.P + inc);
+    cT[lane] = c;
+    int64_t q = 0, q2 = 0;
+    if (valid && t >= 1) fixed_ret(c, cp, q, q2);
+    const int64_t l1 = wave_scan_i64(q, lane);   // |in-tile prefix| <= 64 * 2^56 < 2^63
+    const int64_t l2 = wave_scan_i64(q2, lane);
+    ql[lane] = l1;
+    ql[kTile + lane] = l2;
+    if (lane == 0) {
+        qb[0] = (uint64_t)cy.Q1;
+        qb[1] = (uint64_t)(cy.Q1 >> 64);
+        qb[2] = (uint64_t)cy.Q2;
+        qb[3] = (uint64_t)(cy.Q2 >> 64);
+    }
+    // carries are wave-uniform: keep them in SGPRs
+    cy.P += uniform_i64(__shfl(inc, 63, 64));
+    cy.Q1 += (i128)uniform_i64(__shfl(l1, 63, 64));
+    cy.Q2 += (i128)uniform_i64(__shfl(l2, 63, 64));
+    cy.prevc = __builtin_amdgcn_readfirstlane(__shfl(c, 63, 64));
+    // DST by doubling: S_m / P_m = aggregate from the bar to the end / from the start of its
+    // aligned 2^m block. Level L of the DST is S_L on left halves and P_L on right halves.
+    Agg S = agg_one(c), Pp = S;
+    D[lane] = S;  // level 0
+#pragma unroll
+    for (int m = 1; m < kDstLevels; ++m) {
+        const int half = 1 << (m - 1);
+        const bool left = (lane & half) == 0;
+        // each lane exposes what its partner needs: right-half lanes their prefix, left-half
+        // lanes their suffix; left lanes read the block end, right lanes the block start
+        const Agg expose = agg_sel(left, S, Pp);
+        const int src = left ? (lane | (2 * half - 1)) : (lane & ~(2 * half - 1));
+        const Agg part = shfl_agg(expose, src);
+        S = agg_sel(left, agg_merge(S, part), S);
+        Pp = agg_sel(left, Pp, agg_merge(part, Pp));
+        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
+    }
+}
+
+// Stage 2 for one tile: int32 floor keys for every window (all threads of the block).
+__device__ __forceinline__ void stage_keys(int t0, int B, int nw, int R, const double* ring,
+                                           const int32_t* win, const double* invw, int32_t* K,
+                                           int tid, int nthreads) {
+    for (int idx = tid; idx < nw * kTile; idx += nthreads) {
+        const int w = idx >> 6, b = idx & 63;
+        const int t = t0 + b;
+        const int W = win[w];
+        int32_t key = 0;
+        if (t < B && t + 1 - W >= 0) {
+            const double F = ring[(t + 1) & (R - 1)] - ring[(t + 1 - W) & (R - 1)];  // exact
+            double fl = floor(F * invw[w]);                  // within 1 of floor(F / W)
+            const double r = F - fl * (double)W;             // exact (all terms < 2^53)
+            fl += r < 0.0 ? -1.0 : (r >= (double)W ? 1.0 : 0.0);
+            key = (int32_t)fl;
+        }
+        K[w * kKS + b] = key;
+    }
+}
+
+// Four bars: G = 2G + [x > y], L = 2L + [x < y] per bar. v_cmp writes a lane mask to an SGPR
+// pair and v_addc consumes it as carry-in: 2 VALU per compare instead of cmp+cndmask+shift-or.
+// Masks rotate over four SGPR pairs so each is read >= 2 instructions after its write
+// (gfx950: VALU write of an SGPR -> VALU read as carry needs 2 wait states).
+__device__ __forceinline__ void cmp4(uint32_t& g, uint32_t& l, const int4& x, const int4& y) {
+    uint64_t m0, m1, m2, m3, co;
+    asm volatile(
+        "v_cmp_gt_i32_e64 %[m0], %[x0], %[y0]\n\t"
+        "v_cmp_lt_i32_e64 %[m1], %[x0], %[y0]\n\t"
+        "v_cmp_gt_i32_e64 %[m2], %[x1], %[y1]\n\t"
+        "v_cmp_lt_i32_e64 %[m3], %[x1], %[y1]\n\t"
+        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m0]\n\t"
+        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m1]\n\t"
+        "v_cmp_gt_i32_e64 %[m0], %[x2], %[y2]\n\t"
+        "v_cmp_lt_i32_e64 %[m1], %[x2], %[y2]\n\t"
+        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m2]\n\t"
+        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m3]\n\t"
+        "v_cmp_gt_i32_e64 %[m2], %[x3], %[y3]\n\t"
+        "v_cmp_lt_i32_e64 %[m3], %[x3], %[y3]\n\t"
+        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m0]\n\t"
+        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m1]\n\t"
+        "s_nop 0\n\t"
+        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m2]\n\t"
+        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m3]"
+        : [g] "+v"(g), [l] "+v"(l), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+          [m3] "=&s"(m3), [co] "=&s"(co)
+        : [x0] "v"(x.x), [y0] "v"(y.x), [x1] "v"(x.y), [y1] "v"(y.y), [x2] "v"(x.z),
+          [y2] "v"(y.z), [x3] "v"(x.w), [y3] "v"(y.w));
+}
+
+}  // namespace
 
 template <bool PARITY>
 __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restrict__ syms,
@@ -30,19 +173,22 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nf = g.na, ns = g.nb, nw = nf + ns;
     const int R = g.ring;
-    // LDS carve (every offset a multiple of 16 B)
-    double* ring = reinterpret_cast<double*>(smem);                       // R
-    double* K = ring + R;                                                 // nw * kKeyStride
-    const size_t k_bytes = ((size_t)nw * kKeyStride * 8 + 15) & ~size_t(15);
-    Agg* D = reinterpret_cast<Agg*>(reinterpret_cast<unsigned char*>(K) + k_bytes);  // 6*64
-    uint64_t* Q = reinterpret_cast<uint64_t*>(D + kDstLevels * kTile);     // 4 * 64
-    int32_t* cT = reinterpret_cast<int32_t*>(Q + 4 * kTile);               // 64
-    int32_t* win = cT + kTile;                                             // nw
+    const SmaLds LL = sma_lds_layout(R, nw);
+    double* ring = reinterpret_cast<double*>(smem + LL.ring);
+    int32_t* keys = reinterpret_cast<int32_t*>(smem + LL.keys);
+    double* invw = reinterpret_cast<double*>(smem + LL.invw);
+    int32_t* win = reinterpret_cast<int32_t*>(smem + LL.win);
+    Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
+    int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
+    int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
+    uint64_t* qbs = reinterpret_cast<uint64_t*>(smem + LL.qb);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const bool helper = (tid >> 6) == (int)(blockDim.x >> 6) - 1;  // last wave runs stage 1
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
+    const int ntiles = (B + kTile - 1) / kTile;
     const int P = g.n_params;
     const int p = blockIdx.y * blockDim.x + tid;
     const bool active = p < P;
@@ -50,13 +196,25 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     const int ks = nf + (active ? p % ns : 0);
     const int32_t* crow = close + sd.off;
 
-    for (int w = tid; w < nw; w += blockDim.x) win[w] = w < nf ? g.a[w] : g.b[w - nf];
+    for (int w = tid; w < nw; w += blockDim.x) {
+        const int W = w < nf ? g.a[w] : g.b[w - nf];
+        win[w] = W;
+        invw[w] = 1.0 / (double)W;
+    }
     if (tid == 0) ring[0] = 0.0;
+    __syncthreads();
+    const int fw = win[kf], sw = win[ks];
+    const int warm = (fw > sw ? fw : sw) - 1;  // first decision bar of this lane
 
-    // wave-0 carries across tiles (wave-uniform)
-    int64_t carryP = 0;
-    i128 carryQ1 = 0, carryQ2 = 0;
-    int32_t prevc = 0;
+    ScanCarry cy{0, 0, 0, 0};
+    // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0
+    if (helper) stage_scan(crow, B, 0, lane, R, ring, cts, qls, qbs, dst, cy);
+    __syncthreads();
+    if (helper && ntiles > 1)
+        stage_scan(crow, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile, qbs + 4,
+                   dst + kDstLevels * kTile, cy);
+    stage_keys(0, B, nw, R, ring, win, invw, keys, tid, blockDim.x);
+    __syncthreads();
 
     Acct a;
     acct_init(a);
@@ -64,123 +222,117 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     const size_t gi = (size_t)blockIdx.x * P + p;
     if (PARITY && active) tr = out.trades + gi * out.trade_cap;
 
-    for (int t0 = 0; t0 < B; t0 += kTile) {
-        __syncthreads();
-        if (tid < 64) {  // ---- 1. tile scan (wave 0)
-            const int t = t0 + lane;
-            const bool valid = t < B;
-            const int32_t c = valid ? crow[t] : 0;
-            int32_t cp = __shfl_up(c, 1, 64);
-            if (lane == 0) cp = prevc;
-            const int64_t inc = wave_scan_i64((int64_t)c, lane);
-            ring[(t + 1) & (R - 1)] = (double)(carryP + inc);
-            cT[lane] = valid ? c : 0;
-            int64_t q = 0, q2 = 0;
-            if (valid && t >= 1) fixed_ret(c, cp, q, q2);
-            const i128 Q1 = carryQ1 + wave_scan_i128((i128)q, lane);
-            const i128 Q2 = carryQ2 + wave_scan_i128((i128)q2, lane);
-            Q[lane] = (uint64_t)Q1;
-            Q[kTile + lane] = (uint64_t)(Q1 >> 64);
-            Q[2 * kTile + lane] = (uint64_t)Q2;
-            Q[3 * kTile + lane] = (uint64_t)(Q2 >> 64);
-            carryP += __shfl(inc, 63, 64);
-            carryQ1 = wave_bcast_i128(Q1, 63);
-            carryQ2 = wave_bcast_i128(Q2, 63);
-            prevc = __shfl(c, 63, 64);
+    for (int k = 0; k < ntiles; ++k) {
+        const int t0 = k * kTile;
+        // ---- stage 1 (tile k+2) and stage 2 (tile k+1): independent of stage 3 (tile k)
+        if (helper && k + 2 < ntiles) {
+            const int s = (k + 2) % kStages;
+            stage_scan(crow, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+                       qls + s * 2 * kTile, qbs + s * 4, dst + s * kDstLevels * kTile, cy);
         }
-        __syncthreads();
-        // ---- 2. sparse table + SMA keys (all waves)
-        dst_build(D, cT, tid, blockDim.x);
-        for (int idx = tid; idx < nw * kTile; idx += blockDim.x) {
-            const int w = idx >> 6, b = idx & 63;
-            const int t = t0 + b;
-            const int W = win[w];
-            double k = __builtin_nan("");
-            if (t < B && t + 1 - W >= 0)
-                k = (ring[(t + 1) & (R - 1)] - ring[(t + 1 - W) & (R - 1)]) / (double)W;
-            K[w * kKeyStride + b] = k;
-        }
-        __syncthreads();
-        if (!active) continue;
-        // ---- 3. signal words for 64 bars
-        const double* k1 = K + kf * kKeyStride;
-        const double* k2 = K + ks * kKeyStride;
-        uint32_t g0 = 0, l0 = 0, g1 = 0, l1 = 0;
+        if (k + 1 < ntiles)
+            stage_keys(t0 + kTile, B, nw, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
+                       tid, blockDim.x);
+        // ---- stage 3 (tile k)
+        if (active) {
+            const int s = k % kStages;
+            const int32_t* cT = cts + s * kTile;
+            const int64_t* ql = qls + s * 2 * kTile;
+            const uint64_t* qb = qbs + s * 4;
+            const Agg* D = dst + s * kDstLevels * kTile;
+            const int32_t* K = keys + (k & 1) * nw * kKS;
+            const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
+            const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
+            uint32_t g0 = 0, l0 = 0, g1 = 0, l1 = 0;
 #pragma unroll 1
-        for (int b0 = 0; b0 < 32; b0 += 8) {
+            for (int v0 = 0; v0 < 8; v0 += 4) {
 #pragma unroll
-            for (int b = b0; b < b0 + 8; ++b) {
-                const double x = k1[b], y = k2[b];
-                g0 = (g0 << 1) | (uint32_t)(x > y);
-                l0 = (l0 << 1) | (uint32_t)(x < y);
+                for (int v = v0; v < v0 + 4; ++v) cmp4(g0, l0, k1[v], k2[v]);
             }
-        }
 #pragma unroll 1
-        for (int b0 = 32; b0 < 64; b0 += 8) {
+            for (int v0 = 8; v0 < 16; v0 += 4) {
 #pragma unroll
-            for (int b = b0; b < b0 + 8; ++b) {
-                const double x = k1[b], y = k2[b];
-                g1 = (g1 << 1) | (uint32_t)(x > y);
-                l1 = (l1 << 1) | (uint32_t)(x < y);
+                for (int v = v0; v < v0 + 4; ++v) cmp4(g1, l1, k1[v], k2[v]);
+            }
+            uint64_t G = ((uint64_t)__builtin_bitreverse32(g1) << 32) | __builtin_bitreverse32(g0);
+            uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
+            const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
+            uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
+            const int wb = warm - t0;
+            vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
+            G &= vm;
+            L &= vm;
+            uint64_t T = ~(G | L) & vm;  // equal floor keys: settle exactly
+            while (T) {
+                const int b = __builtin_ctzll(T);
+                T &= T - 1;
+                const int t = t0 + b;
+                const double top = ring[(t + 1) & (R - 1)];
+                const double Fs = (top - ring[(t + 1 - fw) & (R - 1)]) * (double)sw;
+                const double Lf = (top - ring[(t + 1 - sw) & (R - 1)]) * (double)fw;
+                G |= (uint64_t)(Fs > Lf) << b;
+                L |= (uint64_t)(Fs < Lf) << b;
+            }
+            // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
+            uint64_t LONG, SHORT;
+            {
+                const uint64_t A = ~L;
+                const uint64_t s1 = A + G;
+                uint64_t cout = s1 < A;
+                const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
+                cout |= sum < s1;
+                LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
+            }
+            {
+                const uint64_t A = ~G;
+                const uint64_t s1 = A + L;
+                uint64_t cout = s1 < A;
+                const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
+                cout |= sum < s1;
+                SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
+            }
+            const int bl = B - 1 - t0;  // forced exit: flat after bar B-1
+            if (bl < 64) {
+                const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
+                LONG &= keep;
+                SHORT &= keep;
+            }
+            const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
+            const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
+            uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
+            if (F) {
+                const i128 b1 = (i128)(((unsigned __int128)qb[1] << 64) | qb[0]);
+                const i128 b2 = (i128)(((unsigned __int128)qb[3] << 64) | qb[2]);
+                do {  // ---- trade events of this tile, in bar order
+                    const int b = __builtin_ctzll(F);
+                    F &= F - 1;
+                    const int t = t0 + b;
+                    const int32_t cx = cT[b];
+                    const i128 q1 = b1 + (i128)ql[b];
+                    const i128 q2 = b2 + (i128)ql[kTile + b];
+                    if (a.pos != 0) {
+                        const bool here = a.e >= t0;  // trade opened in this tile
+                        const Agg part = dst_query_bf(D, here ? a.e - t0 : 0, b);
+                        const Agg st = agg_sel(here, part, agg_merge(a.agg, part));
+                        acct_close(a, t, cx, st, q1, q2, tr, out.trade_cap);
+                    }
+                    const int np = ((LONG >> b) & 1) ? 1 : (((SHORT >> b) & 1) ? -1 : 0);
+                    if (np != 0) acct_open(a, t, np, cx, q1, q2);
+                } while (F);
+            }
+            if (a.pos != 0) {  // trade continues into the next tile
+                const bool here = a.e >= t0;
+                const Agg part = dst_query_bf(D, here ? a.e - t0 : 0, kTile - 1);
+                a.agg = agg_sel(here, part, agg_merge(a.agg, part));
             }
         }
-        uint64_t G = ((uint64_t)__builtin_bitreverse32(g1) << 32) | __builtin_bitreverse32(g0);
-        uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
-        const int lastdec = B - 2 - t0;  // decisions only at t <= B-2
-        const uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
-        G &= vm;
-        L &= vm;
-        // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
-        uint64_t LONG, SHORT;
-        {
-            const uint64_t A = ~L;
-            const uint64_t s1 = A + G;
-            uint64_t cout = s1 < A;
-            const uint64_t s = s1 + (uint64_t)(a.pos == 1);
-            cout |= s < s1;
-            LONG = ((s ^ A ^ G) >> 1) | (cout << 63);
-        }
-        {
-            const uint64_t A = ~G;
-            const uint64_t s1 = A + L;
-            uint64_t cout = s1 < A;
-            const uint64_t s = s1 + (uint64_t)(a.pos == -1);
-            cout |= s < s1;
-            SHORT = ((s ^ A ^ L) >> 1) | (cout << 63);
-        }
-        const int bl = B - 1 - t0;  // forced exit: flat after bar B-1
-        if (bl < 64) {
-            const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
-            LONG &= keep;
-            SHORT &= keep;
-        }
-        const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
-        const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
-        uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
-        // ---- 4. trade events
-        while (F) {
-            const int b = __builtin_ctzll(F);
-            F &= F - 1;
-            const int t = t0 + b;
-            const int32_t cx = cT[b];
-            const i128 q1 = (i128)(((unsigned __int128)Q[kTile + b] << 64) | Q[b]);
-            const i128 q2 = (i128)(((unsigned __int128)Q[3 * kTile + b] << 64) | Q[2 * kTile + b]);
-            if (a.pos != 0) {
-                const Agg st = a.e >= t0 ? dst_query(D, cT, a.e - t0, b)
-                                         : agg_merge(a.agg, dst_query(D, cT, 0, b));
-                acct_close(a, t, cx, st, q1, q2, tr, out.trade_cap);
-            }
-            const int np = ((LONG >> b) & 1) ? 1 : (((SHORT >> b) & 1) ? -1 : 0);
-            if (np != 0) acct_open(a, t, np, cx, q1, q2);
-        }
-        if (a.pos != 0) {  // trade continues into the next tile
-            a.agg = a.e >= t0 ? dst_query(D, cT, a.e - t0, kTile - 1)
-                              : agg_merge(a.agg, dst_query(D, cT, 0, kTile - 1));
-        }
+        __syncthreads();
     }
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
     wave_add_trades(out, active ? a.ntr : 0);
 }
+
+size_t sma_lds_bytes(const Grid& g) { return sma_lds_layout(g.ring, g.na + g.nb).total; }
 
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                       const Out& out, bool parity, hipStream_t st) {
@@ -188,10 +340,7 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     const int P = g.n_params;
     const int block = P >= kMaxBlock ? kMaxBlock : ((P + 63) / 64) * 64;
     const dim3 grid(n_sym, (P + block - 1) / block);
-    const int nw = g.na + g.nb;
-    const size_t k_bytes = ((size_t)nw * kKeyStride * 8 + 15) & ~size_t(15);
-    const size_t lds = (size_t)g.ring * 8 + k_bytes + kDstLevels * kTile * sizeof(Agg) +
-                       4 * kTile * 8 + kTile * 4 + (size_t)nw * 4;
+    const size_t lds = sma_lds_bytes(g);
     if (parity)
         hipLaunchKernelGGL(sma_kernel<true>, grid, dim3(block), lds, st, syms, close, g, out);
     else
