@@ -90,7 +90,9 @@ struct bt_engine {
     DevBuf<unsigned long long> d_ntr;
     // top-k work
     DevBuf<unsigned int> d_hist, d_counts;
-    DevBuf<unsigned long long> d_state, d_above, d_equal;
+    DevBuf<unsigned long long> d_state, d_above, d_cand;
+    DevBuf<bt_topk_rec> d_top;
+    DevBuf<int32_t> d_topn;
     bool ran = false;
     // timing of the dominant kernel
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
@@ -174,7 +176,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
     e->grid.n_params = e->P;
     if (c.annualization <= 0) return "annualization must be positive";
     e->grid.sqrt_ann = std::sqrt((double)c.annualization);
-    if (c.topk < 0) return "topk must be >= 0";
+    if (c.topk < 0 || c.topk > kTopkMax) return "topk must be in [0, 1024]";
     if ((c.flags & BT_FLAG_PARITY) && c.trade_cap <= 0) return "parity mode needs trade_cap > 0";
     return "";
 }
@@ -228,11 +230,13 @@ void ensure_outputs(bt_engine* e) {
         e->d_trades.ensure(std::max<size_t>(1, n * (size_t)e->cfg.trade_cap));
     }
     if (e->cfg.topk > 0) {
-        e->d_hist.ensure(256);
+        e->d_hist.ensure(4096);
         e->d_counts.ensure(2);
         e->d_state.ensure(4);
-        e->d_above.ensure(std::max<size_t>(1, n));
-        e->d_equal.ensure(std::max<size_t>(1, n));
+        e->d_above.ensure(kTopkCap);
+        e->d_cand.ensure(kTopkCap);
+        e->d_top.ensure(kTopkMax);
+        e->d_topn.ensure(1);
     }
 }
 
@@ -281,8 +285,10 @@ void run_impl(bt_engine* e) {
         e->ev_pending.push_back(ev);
     }
     if (e->cfg.topk > 0) {
-        TopkWork w{e->d_hist.p, e->d_state.p, e->d_counts.p, e->d_above.p, e->d_equal.p};
-        HIPCHK(launch_topk(e->d_key.p, (int64_t)S * e->P, e->cfg.topk, w, e->stream));
+        TopkWork w{e->d_hist.p, e->d_state.p, e->d_counts.p, e->d_above.p, e->d_cand.p,
+                   kTopkCap, e->d_top.p, e->d_topn.p};
+        HIPCHK(launch_topk(e->d_key.p, e->d_sum.p, e->d_syms.p, (int64_t)S * e->P, e->P,
+                           e->cfg.topk, w, e->stream));
     }
     e->ran = true;
 }
@@ -307,25 +313,27 @@ bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b) {  // "a ranks before
 }
 
 std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
-    std::vector<bt_topk_rec> res;
     if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
     HIPCHK(hipStreamSynchronize(e->stream));
-    unsigned int counts[2];
-    unsigned long long state[4];
-    HIPCHK(hipMemcpy(counts, e->d_counts.p, sizeof counts, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(state, e->d_state.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    std::vector<unsigned long long> idx(counts[0] + counts[1]);
-    if (counts[0])
-        HIPCHK(hipMemcpy(idx.data(), e->d_above.p, counts[0] * 8ULL, hipMemcpyDeviceToHost));
-    if (counts[1])
-        HIPCHK(hipMemcpy(idx.data() + counts[0], e->d_equal.p, counts[1] * 8ULL, hipMemcpyDeviceToHost));
-    std::vector<bt_summary> rec(1);
-    for (unsigned long long i : idx) {
-        HIPCHK(hipMemcpy(rec.data(), e->d_sum.p + i, sizeof(bt_summary), hipMemcpyDeviceToHost));
-        const int32_t s = (int32_t)(i / e->P), p = (int32_t)(i % e->P);
-        res.push_back(bt_topk_rec{rec[0].sharpe, e->syms[s].id, p, rec[0].pnl});
+    int32_t n = 0;
+    HIPCHK(hipMemcpy(&n, e->d_topn.p, sizeof n, hipMemcpyDeviceToHost));
+    std::vector<bt_topk_rec> res;
+    if (n >= 0) {
+        res.resize((size_t)n);
+        if (n) HIPCHK(hipMemcpy(res.data(), e->d_top.p, (size_t)n * sizeof(bt_topk_rec), hipMemcpyDeviceToHost));
+    } else {  // more than kTopkCap records tie on the selected prefix: finish on the host
+        const size_t total = e->syms.size() * (size_t)e->P;
+        std::vector<bt_summary> all(total);
+        HIPCHK(hipMemcpy(all.data(), e->d_sum.p, total * sizeof(bt_summary), hipMemcpyDeviceToHost));
+        res.reserve(total);
+        for (size_t i = 0; i < total; ++i) {
+            const int32_t s = (int32_t)(i / e->P), p = (int32_t)(i % e->P);
+            res.push_back(bt_topk_rec{all[i].sharpe, e->syms[s].id, p, all[i].pnl});
+        }
+        const size_t m = std::min<size_t>(res.size(), (size_t)e->cfg.topk);
+        std::partial_sort(res.begin(), res.begin() + m, res.end(), topk_less);
+        res.resize(m);
     }
-    std::sort(res.begin(), res.end(), topk_less);
     if ((int32_t)res.size() > k) res.resize(k);
     return res;
 }
@@ -462,7 +470,9 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_counts.release();
         e->d_state.release();
         e->d_above.release();
-        e->d_equal.release();
+        e->d_cand.release();
+        e->d_top.release();
+        e->d_topn.release();
         if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     } catch (...) {
     }

@@ -58,16 +58,21 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high,
                        const int32_t* low, const int32_t* close, int64_t* q, int64_t* q2,
                        const Grid& g, const Out& out, bool parity, hipStream_t st);
 
-// Top-k by radix select over `key` (n records); writes candidates, host finishes the order.
+// Top-k by radix select over `key` (k_topk.hip): device-side finish into `out`.
+constexpr int kTopkCap = 2048;      // candidates sorted in LDS by the finish kernel
+constexpr int kTopkMax = 1024;      // largest k the engine accepts
 struct TopkWork {
-    unsigned int* hist;            // [256]
-    unsigned long long* state;     // [4]: prefix, mask, remaining k, pad
-    unsigned int* counts;          // [2]: n_above, n_equal
-    unsigned long long* above;     // [n] indices with key > threshold (capacity n)
-    unsigned long long* equal;     // [n] indices with key == threshold
+    unsigned int* hist;            // [4096]
+    unsigned long long* state;     // [4]: prefix, decided-bit mask, remaining need
+    unsigned int* counts;          // [2]: above, candidates
+    unsigned long long* above;     // [cap]
+    unsigned long long* cand;      // [cap]
+    int cap;
+    bt_topk_rec* out;              // [k]
+    int32_t* out_n;                // [1]: records written, -1 = overflow (host finishes)
 };
-hipError_t launch_topk(const uint64_t* key, int64_t n, int32_t k, const TopkWork& w,
-                       hipStream_t st);
+hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms,
+                       int64_t n, int32_t P, int32_t k, const TopkWork& w, hipStream_t st);
 
 // Shared host/device helpers.
 __host__ __device__ inline uint64_t order_key(double x) {

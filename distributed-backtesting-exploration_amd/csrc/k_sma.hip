@@ -225,12 +225,12 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     for (int k = 0; k < ntiles; ++k) {
         const int t0 = k * kTile;
         // ---- stage 1 (tile k+2) and stage 2 (tile k+1): independent of stage 3 (tile k)
-        if (helper && k + 2 < ntiles) {
+        if (helper && k + 2 < ntiles && !(g.ablate & 1)) {
             const int s = (k + 2) % kStages;
             stage_scan(crow, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
                        qls + s * 2 * kTile, qbs + s * 4, dst + s * kDstLevels * kTile, cy);
         }
-        if (k + 1 < ntiles)
+        if (k + 1 < ntiles && !(g.ablate & 2))
             stage_keys(t0 + kTile, B, nw, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
                        tid, blockDim.x);
         // ---- stage 3 (tile k)
@@ -245,12 +245,12 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
             uint32_t g0 = 0, l0 = 0, g1 = 0, l1 = 0;
 #pragma unroll 1
-            for (int v0 = 0; v0 < 8; v0 += 4) {
+            for (int v0 = 0; v0 < 8 && !(g.ablate & 4); v0 += 4) {
 #pragma unroll
                 for (int v = v0; v < v0 + 4; ++v) cmp4(g0, l0, k1[v], k2[v]);
             }
 #pragma unroll 1
-            for (int v0 = 8; v0 < 16; v0 += 4) {
+            for (int v0 = 8; v0 < 16 && !(g.ablate & 4); v0 += 4) {
 #pragma unroll
                 for (int v = v0; v < v0 + 4; ++v) cmp4(g1, l1, k1[v], k2[v]);
             }
@@ -300,6 +300,10 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
             const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
             uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
+            if (g.ablate & 8) {  // profiling: drop the trade events (keep F live)
+                asm volatile("" ::"v"((uint32_t)F), "v"((uint32_t)(F >> 32)));
+                F = 0;
+            }
             if (F) {
                 const i128 b1 = (i128)(((unsigned __int128)qb[1] << 64) | qb[0]);
                 const i128 b2 = (i128)(((unsigned __int128)qb[3] << 64) | qb[2]);

@@ -1,86 +1,185 @@
 // k_topk.hip — per-GPU top-k of (symbol, param) results by Sharpe.
 //
-// Radix select on the 64-bit order key (orderable Sharpe): eight 8-bit digit passes find the
-// k-th largest key K exactly, then one pass collects every record with key > K (< k of them)
-// and every record with key == K. The host orders those few candidates by
-// (sharpe desc, sym asc, param asc); ties at K are resolved there, so the result is exact and
-// deterministic regardless of atomics order.
+// Radix select on the 64-bit order key (orderable Sharpe), two 12-bit digits:
+//   hist(bits 63..52) -> select -> hist(bits 51..40 | prefix) -> select
+//   -> collect: records whose 24-bit prefix is above the selected one (< k of them) and the
+//      candidates that share it -> finish: one block sorts them in LDS by
+//      (key desc, sym asc, param asc) and writes the k result records.
+// Seven small launches, no host round trip; the host reads one count and k records. The order
+// is exact and deterministic (atomics only decide collection order, which the sort removes).
+// If more than kCap records tie on the 24-bit prefix, finish reports overflow (-1) and the
+// host completes the selection from the raw keys.
 #include "internal.h"
 
 namespace bt {
 
-__global__ __launch_bounds__(256) void topk_hist(const uint64_t* __restrict__ key, int64_t n,
-                                                 int shift, const unsigned long long* state,
-                                                 unsigned int* hist) {
-    __shared__ unsigned int h[256];
-    h[threadIdx.x] = 0;
+namespace {
+constexpr int kBins = 4096;
+}
+
+// state: [0] prefix, [1] mask of decided bits, [2] records still needed from the prefix group
+__global__ __launch_bounds__(256) void topk_hist(const uint64_t* __restrict__ key, int64_t n, int shift,
+                                                 const unsigned long long* __restrict__ state,
+                                                 unsigned int* __restrict__ hist) {
+    __shared__ unsigned int h[kBins];
+    for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    const uint64_t prefix = state[0];
-    const uint64_t hi_mask = shift >= 56 ? 0ULL : ~((1ULL << (shift + 8)) - 1);
+    const uint64_t prefix = state[0], mask = state[1];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = key[i];
-        if ((k & hi_mask) == (prefix & hi_mask)) atomicAdd(&h[(k >> shift) & 255], 1u);
+        if ((k & mask) == prefix) atomicAdd(&h[(k >> shift) & (kBins - 1)], 1u);
     }
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+    for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-// One wave: find the digit holding the `need`-th largest key among the current prefix group.
-__global__ void topk_select(int shift, unsigned long long* state, unsigned int* hist) {
-    if (threadIdx.x == 0) {
-        uint64_t need = state[1];
-        uint64_t cum = 0;
-        int d = 255;
-        for (; d > 0; --d) {
-            if (cum + hist[d] >= need) break;
-            cum += hist[d];
+// One block of 256 threads; thread t owns bins 4095-16t .. 4080-16t (counted from the top).
+__global__ __launch_bounds__(256) void topk_select(unsigned int* __restrict__ hist, int shift,
+                                                   unsigned long long* __restrict__ state) {
+    __shared__ unsigned int part[256];
+    const int t = threadIdx.x;
+    const int top = kBins - 1 - 16 * t;
+    unsigned int s = 0;
+    for (int j = 0; j < 16; ++j) s += hist[top - j];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        const unsigned long long need = state[2];
+        unsigned long long cum = 0;
+        int owner = 255;
+        for (int i = 0; i < 256; ++i) {
+            if (cum + part[i] >= need) {
+                owner = i;
+                break;
+            }
+            cum += part[i];
         }
-        state[0] |= (uint64_t)d << shift;
-        state[1] = need - cum;
+        const int b = kBins - 1 - 16 * owner;
+        int bin = b - 15;
+        for (int j = 0; j < 16; ++j) {
+            if (cum + hist[b - j] >= need) {
+                bin = b - j;
+                break;
+            }
+            cum += hist[b - j];
+        }
+        state[0] |= (unsigned long long)bin << shift;
+        state[1] |= (unsigned long long)(kBins - 1) << shift;
+        state[2] = need - cum;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    for (int i = t; i < kBins; i += blockDim.x) hist[i] = 0;  // ready for the next digit
 }
 
 __global__ __launch_bounds__(256) void topk_collect(const uint64_t* __restrict__ key, int64_t n,
-                                                    const unsigned long long* state,
-                                                    unsigned int* counts,
-                                                    unsigned long long* above,
-                                                    unsigned long long* equal) {
-    const uint64_t K = state[0];
+                                                    const unsigned long long* __restrict__ state,
+                                                    unsigned int* __restrict__ counts,
+                                                    unsigned long long* __restrict__ above,
+                                                    unsigned long long* __restrict__ cand, int cap) {
+    const uint64_t prefix = state[0], mask = state[1];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = key[i];
-        if (k > K) above[atomicAdd(&counts[0], 1u)] = (unsigned long long)i;
-        else if (k == K) equal[atomicAdd(&counts[1], 1u)] = (unsigned long long)i;
+        const uint64_t m = key[i] & mask;
+        if (m > prefix) {
+            const unsigned int j = atomicAdd(&counts[0], 1u);
+            if ((int)j < cap) above[j] = (unsigned long long)i;
+        } else if (m == prefix) {
+            const unsigned int j = atomicAdd(&counts[1], 1u);
+            if ((int)j < cap) cand[j] = (unsigned long long)i;
+        }
     }
+}
+
+__global__ __launch_bounds__(1024) void topk_finish(
+    const uint64_t* __restrict__ key, const bt_summary* __restrict__ sum,
+    const SymDesc* __restrict__ syms, int32_t P, const unsigned int* __restrict__ counts,
+    const unsigned long long* __restrict__ above, const unsigned long long* __restrict__ cand,
+    int cap, int32_t k, bt_topk_rec* __restrict__ out, int32_t* __restrict__ out_n) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* kk = reinterpret_cast<uint64_t*>(smem);  // order key (desc)
+    uint64_t* ss = kk + cap;                            // (sym id, param) (asc)
+    uint64_t* ix = ss + cap;                            // record index (payload)
+    const int n_above = (int)counts[0], n_cand = (int)counts[1];
+    const int n = n_above + n_cand;
+    if (n > cap) {
+        if (threadIdx.x == 0) out_n[0] = -1;
+        return;
+    }
+    int m = 1;
+    while (m < n) m <<= 1;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        if (i < n) {
+            const unsigned long long idx = i < n_above ? above[i] : cand[i - n_above];
+            const int s = (int)(idx / (unsigned long long)P), p = (int)(idx % (unsigned long long)P);
+            kk[i] = key[idx];
+            ss[i] = ((uint64_t)(uint32_t)syms[s].id << 32) | (uint32_t)p;
+            ix[i] = idx;
+        } else {  // padding sorts last
+            kk[i] = 0;
+            ss[i] = ~0ULL;
+            ix[i] = 0;
+        }
+    }
+    __syncthreads();
+    for (int size = 2; size <= m; size <<= 1) {  // bitonic: best first
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < m; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const bool i_first = kk[i] > kk[j] || (kk[i] == kk[j] && ss[i] < ss[j]);
+                    if (i_first != up) {
+                        uint64_t t = kk[i];
+                        kk[i] = kk[j];
+                        kk[j] = t;
+                        t = ss[i];
+                        ss[i] = ss[j];
+                        ss[j] = t;
+                        t = ix[i];
+                        ix[i] = ix[j];
+                        ix[j] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int take = n < k ? n : k;
+    for (int i = threadIdx.x; i < take; i += blockDim.x) {
+        const bt_summary& r = sum[ix[i]];
+        out[i] = bt_topk_rec{r.sharpe, (int32_t)(ss[i] >> 32), (int32_t)(uint32_t)ss[i], r.pnl};
+    }
+    if (threadIdx.x == 0) out_n[0] = take;
 }
 
 __global__ void topk_init(unsigned long long* state, unsigned int* counts, unsigned int* hist,
                           unsigned long long need) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[i] = 0;
     if (threadIdx.x == 0) {
-        state[0] = 0;
-        state[1] = need;
+        state[0] = state[1] = 0;
+        state[2] = need;
         counts[0] = counts[1] = 0;
     }
 }
 
-hipError_t launch_topk(const uint64_t* key, int64_t n, int32_t k, const TopkWork& w,
-                       hipStream_t st) {
+hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms, int64_t n,
+                       int32_t P, int32_t k, const TopkWork& w, hipStream_t st) {
     if (n <= 0 || k <= 0) return hipSuccess;
     const unsigned long long need = (unsigned long long)(k < n ? k : n);
+    int64_t blocks = (n + 2047) / 2048;
+    if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(topk_init, dim3(1), dim3(256), 0, st, w.state, w.counts, w.hist, need);
-    int64_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int shift = 52; shift >= 40; shift -= 12) {
         hipLaunchKernelGGL(topk_hist, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
                            (const unsigned long long*)w.state, w.hist);
-        hipLaunchKernelGGL(topk_select, dim3(1), dim3(64), 0, st, shift, w.state, w.hist);
+        hipLaunchKernelGGL(topk_select, dim3(1), dim3(256), 0, st, w.hist, shift, w.state);
     }
     hipLaunchKernelGGL(topk_collect, dim3((unsigned)blocks), dim3(256), 0, st, key, n,
-                       (const unsigned long long*)w.state, w.counts, w.above, w.equal);
+                       (const unsigned long long*)w.state, w.counts, w.above, w.cand, w.cap);
+    hipLaunchKernelGGL(topk_finish, dim3(1), dim3(1024), (size_t)w.cap * 24, st, key, sum, syms,
+                       P, w.counts, w.above, w.cand, w.cap, k, w.out, w.out_n);
     return hipGetLastError();
 }
 

@@ -172,3 +172,16 @@ def test_config2_full_shape_sampled_parity():
                         -flat["sharpe"]))
     exp = [(int(i // grid.n_params), int(i % grid.n_params)) for i in order[:100]]
     assert [(int(t["sym"]), int(t["param"])) for t in top] == exp
+
+
+def test_topk_massive_ties_host_finish():
+    """More records tie on the selected key prefix than the device finish can sort: every
+    Sharpe is 0 on flat prices, so the order is (sym asc, param asc) — the host path."""
+    grid = D.Grid.sma([2, 3, 4], [5, 6, 7], annualization=252)
+    closes = [np.full(200, 1_000_000, np.int32) for _ in range(300)]   # 2,700 records
+    with D.Engine(grid, topk=50) as e:
+        e.load_ohlc(closes, sym_ids=np.arange(1000, 1300))
+        e.run()
+        top = e.read_topk()
+    assert [(int(t["sym"]), int(t["param"])) for t in top] == [(1000 + i // 9, i % 9) for i in range(50)]
+    assert all(float(t["sharpe"]) == 0.0 for t in top)
