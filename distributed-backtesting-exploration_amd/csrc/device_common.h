@@ -36,39 +36,6 @@ __device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) {
     return r;
 }
 
-// Disjoint sparse table over one tile of closes (kTile entries, kDstLevels levels).
-// D[L*kTile + pos]: for level L (blocks of 2^(L+1)), the aggregate from pos to the block
-// middle (left half) or from the middle+1 to pos (right half). Any range [a, b] inside the
-// tile is then one merge of two entries: O(1) per trade, independent of trade length.
-__device__ __forceinline__ void dst_build(Agg* D, const int32_t* cT, int tid, int nthreads) {
-    for (int idx = tid; idx < kDstLevels * kTile; idx += nthreads) {
-        const int L = idx / kTile, pos = idx % kTile;
-        const int half = 1 << L;
-        const int mid = (pos & ~(2 * half - 1)) + half - 1;
-        Agg a;
-        if (pos <= mid) {  // suffix pos..mid, built right-to-left
-            a = agg_one(cT[mid]);
-            for (int q = mid - 1; q >= pos; --q) {
-                const int32_t x = cT[q];
-                a.dd = max(a.dd, x - a.mn);
-                a.du = max(a.du, a.mx - x);
-                a.mx = max(a.mx, x);
-                a.mn = min(a.mn, x);
-            }
-        } else {  // prefix mid+1..pos, built left-to-right
-            a = agg_one(cT[mid + 1]);
-            for (int q = mid + 2; q <= pos; ++q) {
-                const int32_t x = cT[q];
-                a.dd = max(a.dd, a.mx - x);
-                a.du = max(a.du, x - a.mn);
-                a.mx = max(a.mx, x);
-                a.mn = min(a.mn, x);
-            }
-        }
-        D[idx] = a;
-    }
-}
-
 // Aggregate of closes cT[a..b], 0 <= a <= b < kTile.
 __device__ __forceinline__ Agg dst_query(const Agg* D, const int32_t* cT, int a, int b) {
     if (a == b) return agg_one(cT[a]);
@@ -84,120 +51,37 @@ __device__ __forceinline__ Agg dst_query_bf(const Agg* D, int a, int b) {
     return agg_merge(D[L * kTile + a], D[L * kTile + b]);
 }
 
-// Per-lane trade accounting state (spec §4), updated only at trade events.
-// S1/S2 (spec §4) of an open trade are folded in at the entry (-side*Q1[e], -Q2[e]) and the
-// exit (+side*Q1[x], +Q2[x]), so no per-trade prefix value has to stay live in registers.
-struct Acct {
-    int32_t pos, e, ce, ntr, expo;
-    int64_t R, peak, mdd;
-    i128 s1, s2;
-    uint64_t h;
-    Agg agg;  // closes [e, current tile start - 1] while a trade spans tiles
-};
+// Identity of agg_merge: merge(kAggId, x) == x for prices in [1, 2^31) (no int32 overflow:
+// 0 - x.mn < 0 and x.mx - INT32_MAX <= 0).
+constexpr Agg kAggId = {0, 0x7FFFFFFF, 0, 0};
 
-__device__ __forceinline__ void acct_init(Acct& a) {
-    a.pos = 0;
-    a.e = 0;
-    a.ce = 0;
-    a.ntr = 0;
-    a.expo = 0;
-    a.R = a.peak = a.mdd = 0;
-    a.s1 = a.s2 = 0;
-    a.h = kFnvOff;
-    a.agg = Agg{0, 0, 0, 0};
-}
-
-// Close the open trade at bar x (tile offset bx) at price px; `st` = aggregate of the trade's
-// MTM path (closes e..x for a close fill; closes e..x-1 plus the fill for an SL/TP fill).
-__device__ __forceinline__ void acct_close(Acct& a, int x, int64_t px, const Agg& st, i128 q1x,
-                                           i128 q2x, bt_trade* tr, int cap) {
-    int64_t emin, emax, path, pnl;
-    if (a.pos > 0) {
-        emin = a.R + ((int64_t)st.mn - a.ce);
-        emax = a.R + ((int64_t)st.mx - a.ce);
-        path = st.dd;
-        pnl = px - a.ce;
-        a.s1 += q1x;
-    } else {
-        emin = a.R + ((int64_t)a.ce - st.mx);
-        emax = a.R + ((int64_t)a.ce - st.mn);
-        path = st.du;
-        pnl = (int64_t)a.ce - px;
-        a.s1 -= q1x;
+// Wave64 inclusive scan of int64 with DPP (row_shr 1,2,4,8 inside 16-lane rows, then
+// row_bcast15 / row_bcast31 across rows): no LDS round trip.
+__device__ __forceinline__ int64_t wave_iscan_i64(int64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)((uint64_t)x >> 32);
+#define BT_DPP_STEP(ctrl, rmask)                                                      \
+    {                                                                                 \
+        const uint32_t ylo = __builtin_amdgcn_update_dpp(0u, lo, ctrl, rmask, 0xf, false); \
+        const uint32_t yhi = __builtin_amdgcn_update_dpp(0u, hi, ctrl, rmask, 0xf, false); \
+        const uint64_t r = (((uint64_t)hi << 32) | lo) + (((uint64_t)yhi << 32) | ylo);   \
+        lo = (uint32_t)r;                                                             \
+        hi = (uint32_t)(r >> 32);                                                     \
     }
-    a.s2 += q2x;
-    a.mdd = max(a.mdd, max(a.peak - emin, path));
-    a.peak = max(a.peak, emax);
-    a.R += pnl;
-    a.expo += x - a.e;
-    const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)x << 31) |
-                       ((uint64_t)(a.pos > 0) << 62);
-    a.h = (a.h ^ w) * kFnvPrime;
-    if (tr != nullptr && a.ntr < cap) {
-        bt_trade r;
-        r.entry_bar = a.e;
-        r.exit_bar = x;
-        r.side = a.pos;
-        r.pad = 0;
-        r.entry_px = a.ce;
-        r.exit_px = px;
-        tr[a.ntr] = r;
-    }
-    a.ntr++;
-    a.pos = 0;
+    BT_DPP_STEP(0x111, 0xf)  // row_shr:1
+    BT_DPP_STEP(0x112, 0xf)  // row_shr:2
+    BT_DPP_STEP(0x114, 0xf)  // row_shr:4
+    BT_DPP_STEP(0x118, 0xf)  // row_shr:8
+    BT_DPP_STEP(0x142, 0xa)  // row_bcast:15 into rows 1, 3
+    BT_DPP_STEP(0x143, 0xc)  // row_bcast:31 into rows 2, 3
+#undef BT_DPP_STEP
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ void acct_open(Acct& a, int t, int side, int32_t ce, i128 q1, i128 q2) {
-    a.pos = side;
-    a.e = t;
-    a.ce = ce;
-    if (side > 0) a.s1 -= q1;
-    else a.s1 += q1;
-    a.s2 -= q2;
-}
-
-__device__ __forceinline__ void acct_write(const Acct& a, int bars, double sqrt_ann, size_t gi,
-                                           const Out& out) {
-    const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
-    const int64_t s1hi = (int64_t)(a.s1 >> 64), s2hi = (int64_t)(a.s2 >> 64);
-    const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, bars, sqrt_ann);
-    bt_summary r;
-    r.n_trades = a.ntr;
-    r.status = 0;
-    r.pnl = a.R;
-    r.mdd = a.mdd;
-    r.exposure = a.expo;
-    r.sharpe = sh;
-    r.hash = a.h;
-    out.sum[gi] = r;
-    out.key[gi] = order_key(sh);
-    if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
-}
-
-// Wave-wide inclusive scans (wave64).
-__device__ __forceinline__ int64_t wave_scan_i64(int64_t x, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-
-__device__ __forceinline__ i128 wave_scan_i128(i128 x, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t lo = __shfl_up((unsigned long long)(uint64_t)x, d, 64);
-        const int64_t hi = __shfl_up((long long)(int64_t)(x >> 64), d, 64);
-        if (lane >= d) x += (i128)(((unsigned __int128)(uint64_t)hi << 64) | lo);
-    }
-    return x;
-}
-
-__device__ __forceinline__ i128 wave_bcast_i128(i128 x, int src) {
-    const uint64_t lo = __shfl((unsigned long long)(uint64_t)x, src, 64);
-    const uint64_t hi = __shfl((unsigned long long)(uint64_t)(x >> 64), src, 64);
-    return (i128)(((unsigned __int128)hi << 64) | lo);
+// Value of lane 63 as a wave-uniform (SGPR) int64.
+__device__ __forceinline__ int64_t lane63_i64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)x >> 32), 63);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // q_t and q2_t of spec §3 for one bar.

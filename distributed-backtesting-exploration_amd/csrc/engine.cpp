@@ -87,7 +87,7 @@ struct bt_engine {
     DevBuf<uint64_t> d_key;
     DevBuf<bt_sums> d_sums;
     DevBuf<bt_trade> d_trades;
-    DevBuf<unsigned long long> d_ntr;
+    DevBuf<unsigned long long> d_ntr, d_dbg;
     // top-k work
     DevBuf<unsigned int> d_hist, d_counts;
     DevBuf<unsigned long long> d_state, d_above, d_cand;
@@ -253,6 +253,12 @@ void run_impl(bt_engine* e) {
     out.trade_cap = parity ? e->cfg.trade_cap : 0;
     out.n_trades = e->d_ntr.p;
     HIPCHK(hipMemsetAsync(e->d_ntr.p, 0, sizeof(unsigned long long), e->stream));
+    out.dbg = nullptr;
+    if (e->grid.ablate & 64) {  // profiling stamps
+        e->d_dbg.ensure(32);
+        HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, 32 * sizeof(unsigned long long), e->stream));
+        out.dbg = e->d_dbg.p;
+    }
     const bool timing = (e->cfg.flags & BT_FLAG_TIMING) != 0;
     std::pair<hipEvent_t, hipEvent_t> ev{};
     if (timing) {
@@ -466,6 +472,7 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_sums.release();
         e->d_trades.release();
         e->d_ntr.release();
+        e->d_dbg.release();
         e->d_hist.release();
         e->d_counts.release();
         e->d_state.release();
@@ -618,6 +625,16 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n) 
         activate(e);
         HIPCHK(hipStreamSynchronize(e->stream));
         HIPCHK(hipMemcpy(out, e->d_c.p + sd.off, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return 0;
+    })
+}
+
+int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n) {
+    ABI_GUARD(-1, {
+        if (!e || !out || n < 0 || n > 32 || !e->d_dbg.p) throw HipFail{"no debug stamps"};
+        activate(e);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d_dbg.p, (size_t)n * 8, hipMemcpyDeviceToHost));
         return 0;
     })
 }

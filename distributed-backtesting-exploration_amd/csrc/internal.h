@@ -42,6 +42,7 @@ struct Out {
     bt_trade* trades;              // [S * P * trade_cap] parity mode, else nullptr
     int32_t trade_cap;
     unsigned long long* n_trades;  // total trades (one atomic per block)
+    unsigned long long* dbg;       // profiling stamps (Grid::ablate & 64), else nullptr
 };
 
 // Launchers (k_*.hip). All enqueue on `st` and return hipError_t.

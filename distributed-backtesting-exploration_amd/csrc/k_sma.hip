@@ -6,7 +6,7 @@
 //
 // HBM is read once (4 B of close per bar per symbol); everything else lives in LDS, one 64-bar
 // tile at a time, in a three-stage software pipeline with ONE workgroup barrier per tile:
-//   stage 1, tile k+2 (the last wave, "helper"): exact int64 prefix of close appended to a ring
+//   stage 1, tile k+2 (a dedicated helper wave): exact int64 prefix of close appended to a ring
 //            of doubles (exact below 2^53); fixed-point returns q, q2 (spec §3) and their
 //            in-tile int64 prefixes + int128 tile base; the tile's disjoint sparse table (DST) of
 //            the close path (max, min, drawdown, draw-up), built by log-doubling shuffles.
@@ -19,6 +19,8 @@
 //            bit-parallel: a set/reset latch is an add-with-carry (LONG = carries of
 //            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
 //            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
+#include <algorithm>
+
 #include "device_common.h"
 
 namespace bt {
@@ -29,7 +31,7 @@ constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned
 constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
 
 struct SmaLds {                       // byte offsets into dynamic LDS
-    size_t ring, keys, invw, win, dst, ct, ql, qb, total;
+    size_t ring, keys, invw, win, dst, ct, ql, total;
 };
 
 __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
@@ -43,7 +45,6 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
-    L.qb = take((size_t)kStages * 4 * 8);
     L.total = o;
     return L;
 }
@@ -54,47 +55,30 @@ __device__ __forceinline__ Agg shfl_agg(const Agg& a, int src) {
                __shfl(a.du, src, 64)};
 }
 
-__device__ __forceinline__ int64_t uniform_i64(int64_t x) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
 // Stage 1 for one tile, executed by one whole wave (lane = bar of the tile).
 struct ScanCarry {
     int64_t P;          // sum of closes before the tile
-    i128 Q1, Q2;        // sum of q, q2 before the tile
     int32_t prevc;      // close of the bar before the tile
 };
 
 __device__ __forceinline__ void stage_scan(const int32_t* __restrict__ crow, int B, int t0, int lane,
-                                           int R, double* ring, int32_t* cT, int64_t* ql,
-                                           uint64_t* qb, Agg* D, ScanCarry& cy) {
+                                           int R, double* ring, int32_t* cT, int64_t* ql, Agg* D,
+                                           ScanCarry& cy) {
     const int t = t0 + lane;
     const bool valid = t < B;
     const int32_t c = valid ? crow[t] : 0;
-    int32_t cp = __shfl_up(c, 1, 64);
-    if (lane == 0) cp = cy.prevc;
-    const int64_t inc = wave_scan_i64((int64_t)c, lane);
+    // previous bar's close: DPP wave_shr:1, lane 0 takes the carry
+    const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
+                                                            0x138, 0xf, 0xf, false);
+    const int64_t inc = wave_iscan_i64((int64_t)c);
     ring[(t + 1) & (R - 1)] = (double)(cy.P + inc);
     cT[lane] = c;
     int64_t q = 0, q2 = 0;
     if (valid && t >= 1) fixed_ret(c, cp, q, q2);
-    const int64_t l1 = wave_scan_i64(q, lane);   // |in-tile prefix| <= 64 * 2^56 < 2^63
-    const int64_t l2 = wave_scan_i64(q2, lane);
-    ql[lane] = l1;
-    ql[kTile + lane] = l2;
-    if (lane == 0) {
-        qb[0] = (uint64_t)cy.Q1;
-        qb[1] = (uint64_t)(cy.Q1 >> 64);
-        qb[2] = (uint64_t)cy.Q2;
-        qb[3] = (uint64_t)(cy.Q2 >> 64);
-    }
-    // carries are wave-uniform: keep them in SGPRs
-    cy.P += uniform_i64(__shfl(inc, 63, 64));
-    cy.Q1 += (i128)uniform_i64(__shfl(l1, 63, 64));
-    cy.Q2 += (i128)uniform_i64(__shfl(l2, 63, 64));
-    cy.prevc = __builtin_amdgcn_readfirstlane(__shfl(c, 63, 64));
+    ql[lane] = wave_iscan_i64(q);              // in-tile prefix: |.| <= 64 * 2^56 < 2^63
+    ql[kTile + lane] = wave_iscan_i64(q2);
+    cy.P += lane63_i64(inc);
+    cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
     // DST by doubling: S_m / P_m = aggregate from the bar to the end / from the start of its
     // aligned 2^m block. Level L of the DST is S_L on left halves and P_L on right halves.
     Agg S = agg_one(c), Pp = S;
@@ -166,7 +150,71 @@ __device__ __forceinline__ void cmp4(uint32_t& g, uint32_t& l, const int4& x, co
 
 }  // namespace
 
+// Per-lane trade accounting (spec §4), touched only at position flips.
+//  * drawdown via gap = peak - realized (int64 >= 0): a closed trade with MTM range
+//    [R+lo, R+hi] and path drawdown `path` gives mdd = max(mdd, gap - lo, path) and
+//    gap' = max(gap, hi) - pnl;
+//  * S1/S2 via per-tile partial sums of the in-tile return prefix (uint64, exact modulo 2^64;
+//    each tile's true total is a masked sum of <= 64 q's, |.| < 2^63), folded into int128 at
+//    the tile end: entry at bar b adds -side*QL[b], exit adds +side*QL[b], an open position
+//    at the tile end adds +side*QL[63].
+struct SmaAcct {
+    int32_t pos, e, ce, ntr, expo;
+    int64_t R, gap, mdd;
+    uint64_t ps1, ps2, h;
+    i128 s1, s2;
+    Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
+};
+
 template <bool PARITY>
+__device__ __forceinline__ void sma_flip(SmaAcct& a, int b, int t0, int bl, uint64_t LONG,
+                                         const int32_t* cT, const int64_t* ql, const Agg* D,
+                                         bt_trade* tr, int cap) {
+    const int t = t0 + b;
+    const int32_t cx = cT[b];
+    const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
+    if (a.pos != 0) {
+        const int start = a.e >= t0 ? a.e - t0 : 0;
+        const Agg st = agg_merge(a.agg, dst_query_bf(D, start, b));
+        const bool lg = a.pos > 0;
+        const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
+        const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
+        const int32_t path = lg ? st.dd : st.du;
+        const int32_t pnl = lg ? cx - a.ce : a.ce - cx;
+        a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+        a.gap = max(a.gap, (int64_t)hi) - pnl;
+        a.R += pnl;
+        a.ps1 += lg ? qx : (uint64_t)0 - qx;
+        a.ps2 += q2x;
+        a.expo += t - a.e;
+        const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
+                           ((uint64_t)lg << 62);
+        a.h = (a.h ^ w) * kFnvPrime;
+        if (PARITY && a.ntr < cap) {
+            bt_trade r;
+            r.entry_bar = a.e;
+            r.exit_bar = t;
+            r.side = a.pos;
+            r.pad = 0;
+            r.entry_px = a.ce;
+            r.exit_px = cx;
+            tr[a.ntr] = r;
+        }
+        a.ntr++;
+    }
+    // SMA: after the first decision every flip reverses; the forced exit at B-1 goes flat
+    const int np = b == bl ? 0 : (a.pos != 0 ? -a.pos : (((LONG >> b) & 1) ? 1 : -1));
+    if (np != 0) {
+        a.e = t;
+        a.ce = cx;
+        a.agg = kAggId;
+        a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
+        a.ps2 -= q2x;
+    }
+    a.pos = np;
+}
+
+template <bool PARITY, bool STAMPS>
 __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
                                                         Grid g, Out out) {
@@ -181,17 +229,18 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
-    uint64_t* qbs = reinterpret_cast<uint64_t*>(smem + LL.qb);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const bool helper = (tid >> 6) == (int)(blockDim.x >> 6) - 1;  // last wave runs stage 1
+    // the last wave is a dedicated helper: stage 1 only, no parameter lanes
+    const int nparam_threads = (int)blockDim.x - 64;
+    const bool helper = tid >= nparam_threads;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
     const int ntiles = (B + kTile - 1) / kTile;
     const int P = g.n_params;
-    const int p = blockIdx.y * blockDim.x + tid;
-    const bool active = p < P;
+    const int p = blockIdx.y * nparam_threads + tid;
+    const bool active = !helper && p < P;
     const int kf = active ? p / ns : 0;
     const int ks = nf + (active ? p % ns : 0);
     const int32_t* crow = close + sd.off;
@@ -206,21 +255,39 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     const int fw = win[kf], sw = win[ks];
     const int warm = (fw > sw ? fw : sw) - 1;  // first decision bar of this lane
 
-    ScanCarry cy{0, 0, 0, 0};
+    ScanCarry cy{0, 0};
     // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0
-    if (helper) stage_scan(crow, B, 0, lane, R, ring, cts, qls, qbs, dst, cy);
+    if (helper) stage_scan(crow, B, 0, lane, R, ring, cts, qls, dst, cy);
     __syncthreads();
     if (helper && ntiles > 1)
-        stage_scan(crow, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile, qbs + 4,
+        stage_scan(crow, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile,
                    dst + kDstLevels * kTile, cy);
-    stage_keys(0, B, nw, R, ring, win, invw, keys, tid, blockDim.x);
+    if (!helper) stage_keys(0, B, nw, R, ring, win, invw, keys, tid, nparam_threads);
     __syncthreads();
 
-    Acct a;
-    acct_init(a);
+    SmaAcct a;
+    a.pos = a.e = a.ce = a.ntr = a.expo = 0;
+    a.R = a.gap = a.mdd = 0;
+    a.ps1 = a.ps2 = 0;
+    a.h = kFnvOff;
+    a.s1 = a.s2 = 0;
+    a.agg = kAggId;
     bt_trade* tr = nullptr;
     const size_t gi = (size_t)blockIdx.x * P + p;
     if (PARITY && active) tr = out.trades + gi * out.trade_cap;
+    const int cap = out.trade_cap;
+
+    // profiling stamps (diagnostic only: Grid::ablate & 64); wave-uniform sums in SGPRs
+    constexpr bool stamps = STAMPS;  // separate diagnostic instantiation
+    uint64_t st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_prev = 0;
+#define BT_STAMP(i)                                             \
+    if (stamps) {                                               \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+        st_acc[i] += now_ - st_prev;                            \
+        st_prev = now_;                                         \
+    }
+    if (stamps) st_prev = __builtin_amdgcn_s_memtime();
 
     for (int k = 0; k < ntiles; ++k) {
         const int t0 = k * kTile;
@@ -228,17 +295,18 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
         if (helper && k + 2 < ntiles && !(g.ablate & 1)) {
             const int s = (k + 2) % kStages;
             stage_scan(crow, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
-                       qls + s * 2 * kTile, qbs + s * 4, dst + s * kDstLevels * kTile, cy);
+                       qls + s * 2 * kTile, dst + s * kDstLevels * kTile, cy);
         }
-        if (k + 1 < ntiles && !(g.ablate & 2))
+        BT_STAMP(0)
+        if (!helper && k + 1 < ntiles && !(g.ablate & 2))
             stage_keys(t0 + kTile, B, nw, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
-                       tid, blockDim.x);
+                       tid, nparam_threads);
+        BT_STAMP(1)
         // ---- stage 3 (tile k)
         if (active) {
             const int s = k % kStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
-            const uint64_t* qb = qbs + s * 4;
             const Agg* D = dst + s * kDstLevels * kTile;
             const int32_t* K = keys + (k & 1) * nw * kKS;
             const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
@@ -254,6 +322,7 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
 #pragma unroll
                 for (int v = v0; v < v0 + 4; ++v) cmp4(g1, l1, k1[v], k2[v]);
             }
+            BT_STAMP(2)
             uint64_t G = ((uint64_t)__builtin_bitreverse32(g1) << 32) | __builtin_bitreverse32(g0);
             uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
             const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
@@ -299,40 +368,61 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             }
             const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
             const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
-            uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
+            const uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
+            BT_STAMP(3)
+            uint32_t flo = (uint32_t)F, fhi = (uint32_t)(F >> 32);
             if (g.ablate & 8) {  // profiling: drop the trade events (keep F live)
-                asm volatile("" ::"v"((uint32_t)F), "v"((uint32_t)(F >> 32)));
-                F = 0;
+                asm volatile("" ::"v"(flo), "v"(fhi));
+                flo = fhi = 0;
             }
-            if (F) {
-                const i128 b1 = (i128)(((unsigned __int128)qb[1] << 64) | qb[0]);
-                const i128 b2 = (i128)(((unsigned __int128)qb[3] << 64) | qb[2]);
-                do {  // ---- trade events of this tile, in bar order
-                    const int b = __builtin_ctzll(F);
-                    F &= F - 1;
-                    const int t = t0 + b;
-                    const int32_t cx = cT[b];
-                    const i128 q1 = b1 + (i128)ql[b];
-                    const i128 q2 = b2 + (i128)ql[kTile + b];
-                    if (a.pos != 0) {
-                        const bool here = a.e >= t0;  // trade opened in this tile
-                        const Agg part = dst_query_bf(D, here ? a.e - t0 : 0, b);
-                        const Agg st = agg_sel(here, part, agg_merge(a.agg, part));
-                        acct_close(a, t, cx, st, q1, q2, tr, out.trade_cap);
-                    }
-                    const int np = ((LONG >> b) & 1) ? 1 : (((SHORT >> b) & 1) ? -1 : 0);
-                    if (np != 0) acct_open(a, t, np, cx, q1, q2);
-                } while (F);
+            while (flo) {  // ---- trade events of this tile, in bar order
+                const int b = __builtin_ctz(flo);
+                flo &= flo - 1;
+                sma_flip<PARITY>(a, b, t0, bl, LONG, cT, ql, D, tr, cap);
             }
-            if (a.pos != 0) {  // trade continues into the next tile
-                const bool here = a.e >= t0;
-                const Agg part = dst_query_bf(D, here ? a.e - t0 : 0, kTile - 1);
-                a.agg = agg_sel(here, part, agg_merge(a.agg, part));
+            while (fhi) {
+                const int b = 32 + __builtin_ctz(fhi);
+                fhi &= fhi - 1;
+                sma_flip<PARITY>(a, b, t0, bl, LONG, cT, ql, D, tr, cap);
             }
+            BT_STAMP(4)
+            if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
+                const int start = a.e >= t0 ? a.e - t0 : 0;
+                a.agg = agg_merge(a.agg, dst_query_bf(D, start, kTile - 1));
+                const uint64_t q63 = (uint64_t)ql[kTile - 1];
+                a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
+                a.ps2 += (uint64_t)ql[2 * kTile - 1];
+            }
+            a.s1 += (i128)(int64_t)a.ps1;
+            a.s2 += (i128)(int64_t)a.ps2;
+            a.ps1 = a.ps2 = 0;
+            BT_STAMP(5)
         }
         __syncthreads();
+        BT_STAMP(6)
     }
-    if (active) acct_write(a, B, g.sqrt_ann, gi, out);
+#undef BT_STAMP
+    if (stamps && lane == 0) {
+        unsigned long long* d = out.dbg + (helper ? 8 : 0);
+        for (int i = 0; i < 7; ++i) atomicAdd(&d[i], (unsigned long long)st_acc[i]);
+        atomicAdd(&d[7], 1ULL);
+    }
+    if (active) {
+        const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
+        const int64_t s1hi = (int64_t)(a.s1 >> 64), s2hi = (int64_t)(a.s2 >> 64);
+        const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, B, g.sqrt_ann);
+        bt_summary r;
+        r.n_trades = a.ntr;
+        r.status = 0;
+        r.pnl = a.R;
+        r.mdd = a.mdd;
+        r.exposure = a.expo;
+        r.sharpe = sh;
+        r.hash = a.h;
+        out.sum[gi] = r;
+        out.key[gi] = order_key(sh);
+        if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
+    }
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
@@ -342,13 +432,17 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
                       const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
     const int P = g.n_params;
-    const int block = P >= kMaxBlock ? kMaxBlock : ((P + 63) / 64) * 64;
-    const dim3 grid(n_sym, (P + block - 1) / block);
+    // parameter waves (<= 7) plus one helper wave per workgroup
+    const int pw = std::min((P + 63) / 64, kMaxBlock / 64 - 1);
+    const int block = 64 * (pw + 1);
+    const dim3 grid(n_sym, (P + 64 * pw - 1) / (64 * pw));
     const size_t lds = sma_lds_bytes(g);
-    if (parity)
-        hipLaunchKernelGGL(sma_kernel<true>, grid, dim3(block), lds, st, syms, close, g, out);
+    if (g.ablate & 64)
+        hipLaunchKernelGGL((sma_kernel<false, true>), grid, dim3(block), lds, st, syms, close, g, out);
+    else if (parity)
+        hipLaunchKernelGGL((sma_kernel<true, false>), grid, dim3(block), lds, st, syms, close, g, out);
     else
-        hipLaunchKernelGGL(sma_kernel<false>, grid, dim3(block), lds, st, syms, close, g, out);
+        hipLaunchKernelGGL((sma_kernel<false, false>), grid, dim3(block), lds, st, syms, close, g, out);
     return hipGetLastError();
 }
 

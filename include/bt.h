@@ -155,6 +155,9 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n);
 /* Average device time of the dominant kernel (BT_FLAG_TIMING), and how many launches. */
 int32_t bt_kernel_timing(bt_engine* e, double* total_ms, int64_t* launches, const char** name);
 int32_t bt_reset_timing(bt_engine* e);
+/* Profiling aid: per-phase s_memtime sums of the last run when the engine was created with
+ * BT_ABLATE=64 in the environment (developer use; n <= 32). */
+int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n);
 
 /* ---- top-k merge (host): merge sorted record lists from several shards (RCCL gather). */
 int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* out);
