@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import dbx_amd as D  # noqa: E402
+from dbx_amd import parallel as PAR  # noqa: E402
 
 S_PER_GPU, BARS, SEED, TOPK = 5000, 2520, 0x5EED, 100
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -35,21 +36,33 @@ def algorithmic_bytes(S, B, P, c=1, W=40):
     return S * B * (8 * c + 16 * W) + 32 * S * P
 
 
-def cpu_baseline(grid, n_sym=320, threads=None):
-    """The C oracle (scalar, multithreaded: SURVEY B4) on a bounded sample of the same workload."""
+def cpu_baseline(grid, threads=None, target_cpu_s=15.0):
+    """The C oracle (scalar, multithreaded: SURVEY B4) on a bounded sample of the same workload:
+    a 64-symbol probe sizes the sample to ~target_cpu_s thread-seconds (at most all 5,000)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc_ffi as F
     threads = threads or min(16, os.cpu_count() or 1)
-    closes = np.stack([F.gen(SEED, s, BARS, 0)[3] for s in range(n_sym)])
     fast, slow = np.asarray(grid.axes[0]), np.asarray(grid.axes[1])
-    t0 = time.perf_counter()
-    F.sma_grid_mt(closes, fast, slow, 252, threads)
-    dt = time.perf_counter() - t0
+
+    def timed(n):
+        closes = np.stack([F.gen(SEED, s, BARS, 0)[3] for s in range(n)])
+        t0 = time.perf_counter()
+        F.sma_grid_mt(closes, fast, slow, 252, threads)
+        return time.perf_counter() - t0
+
+    probe = 64
+    dt = timed(probe)
+    n_sym = int(min(S_PER_GPU, max(probe, probe * target_cpu_s / threads / max(dt, 1e-6))))
+    if n_sym > probe:
+        dt = timed(n_sym)
+    else:
+        n_sym = probe
     evals = n_sym * BARS * grid.n_params
     return {"value": evals / dt, "unit": "bar-evals/s", "cores": threads, "kind": "port",
             "sample": f"first {n_sym} of the 5000 config-2 symbols x {BARS} bars x "
-                      f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall, "
-                      f"oracle/oracle.c orc_sma_grid_mt, gcc -O2 -ffp-contract=off)"}
+                      f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall on "
+                      f"{threads} threads = {dt * threads:.1f} thread-s; oracle/oracle.c "
+                      f"orc_sma_grid_mt, gcc -O2 -ffp-contract=off)"}
 
 
 def load_traffic():
@@ -91,14 +104,10 @@ def main():
         top = eng.read_topk()          # syncs the engine stream
         if dist is None:
             return top
-        import torch
-        t = torch.from_numpy(top.view(np.int64).reshape(-1, 3).copy()).cuda()
-        bufs = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(bufs, t)      # RCCL over xGMI: k x 24 B per rank
-        cnt = torch.tensor([eng.stats()["trades"]], dtype=torch.int64, device="cuda")
-        dist.all_reduce(cnt)
-        merged = np.concatenate([b.cpu().numpy().reshape(-1).view(D.TOPK_DTYPE) for b in bufs])
-        return D.merge_topk(merged, TOPK)
+        # the one exchange step: RCCL all-gather of k x 24 B per rank + counter all-reduce
+        top = PAR.gather_topk(top, TOPK, dist)
+        PAR.allreduce_counters([S_PER_GPU * BARS * P, eng.stats()["trades"]], dist)
+        return top
 
     for _ in range(args.warmup):
         step()

@@ -370,19 +370,15 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
             const uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
             BT_STAMP(3)
-            uint32_t flo = (uint32_t)F, fhi = (uint32_t)(F >> 32);
+            uint64_t Fw = F;
             if (g.ablate & 8) {  // profiling: drop the trade events (keep F live)
-                asm volatile("" ::"v"(flo), "v"(fhi));
-                flo = fhi = 0;
+                asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
+                Fw = 0;
             }
-            while (flo) {  // ---- trade events of this tile, in bar order
-                const int b = __builtin_ctz(flo);
-                flo &= flo - 1;
-                sma_flip<PARITY>(a, b, t0, bl, LONG, cT, ql, D, tr, cap);
-            }
-            while (fhi) {
-                const int b = 32 + __builtin_ctz(fhi);
-                fhi &= fhi - 1;
+            // one loop over the 64-bit word: a wave iterates max(flips per lane) times
+            while (Fw) {  // ---- trade events of this tile, in bar order
+                const int b = __builtin_ctzll(Fw);
+                Fw &= Fw - 1;
                 sma_flip<PARITY>(a, b, t0, bl, LONG, cT, ql, D, tr, cap);
             }
             BT_STAMP(4)

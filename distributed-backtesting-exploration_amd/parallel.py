@@ -1,0 +1,54 @@
+"""Multi-GPU layout of the hot path: one process per GPU, symbols sharded in
+contiguous blocks, no data-path collective. The only exchange is at the end of a step:
+an all-gather of every rank's top-k records (k x 24 B) and an all-reduce of the run counters,
+over torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in CPU tests).
+
+The reference has one parallelism strategy — file-level job farming, each worker taking whole
+files (/root/reference/src/server/main.rs:131-143) — and no collectives at all; this module is
+the MI355X-native replacement for scale-out inside one node.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import TOPK_DTYPE, merge_topk
+
+
+def shard(n_symbols: int, world: int, rank: int) -> tuple:
+    """Contiguous block of symbols for `rank`: S_g = ceil(S / G) (the last block may be short)."""
+    per = -(-n_symbols // world)
+    begin = min(rank * per, n_symbols)
+    return begin, max(0, min(per, n_symbols - begin))
+
+
+def _device_for(dist):
+    import torch
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
+        else torch.device("cpu")
+
+
+def gather_topk(local: np.ndarray, k: int, dist) -> np.ndarray:
+    """All-gather every rank's top-k records and merge them with the engine's order
+    (sharpe desc, sym asc, param asc). Ranks may hold fewer than k records."""
+    import torch
+    world = dist.get_world_size()
+    buf = np.zeros(k, TOPK_DTYPE)
+    n = min(len(local), k)
+    buf[:n] = np.asarray(local, TOPK_DTYPE)[:n]
+    dev = _device_for(dist)
+    t = torch.from_numpy(buf.view(np.int64).reshape(k, 3).copy()).to(dev)
+    cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+    bufs = [torch.empty_like(t) for _ in range(world)]
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(bufs, t)
+    dist.all_gather(cnts, cnt)
+    parts = [b.cpu().numpy().reshape(-1).view(TOPK_DTYPE)[:int(c.item())] for b, c in zip(bufs, cnts)]
+    return merge_topk(np.concatenate(parts) if parts else np.zeros(0, TOPK_DTYPE), k)
+
+
+def allreduce_counters(values, dist) -> list:
+    """Sum int64 run counters (bar-evals, trades, errors) over all ranks."""
+    import torch
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=_device_for(dist))
+    dist.all_reduce(t)
+    return [int(x) for x in t.cpu().tolist()]

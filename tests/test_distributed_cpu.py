@@ -1,0 +1,83 @@
+"""The N>1 path on CPU: world_size-2 gloo processes run the shard -> local top-k -> all-gather
+-> merge exchange of dbx_amd.parallel and must reproduce the single-process global top-k.
+
+Per-rank results come from the C oracle (test infrastructure) because this container has no
+GPU; on the box the same functions carry engine results over RCCL (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from dbx_amd import parallel as PAR
+
+S, BARS, K = 23, 300, 17
+FAST, SLOW = np.array([4, 8, 12], np.int32), np.array([30, 50], np.int32)
+
+
+def _all_results(sym_ids):
+    import orc_ffi as F
+    closes = np.stack([F.gen(7, int(s), BARS, 0)[3] for s in sym_ids])
+    res = F.sma_grid_mt(closes, FAST, SLOW, 252, 2)
+    recs = np.zeros(res.size, D.TOPK_DTYPE)
+    P = res.shape[1]
+    recs["sharpe"] = res["sharpe"].reshape(-1)
+    recs["pnl"] = res["pnl"].reshape(-1)
+    recs["sym"] = np.repeat(np.asarray(sym_ids), P)
+    recs["param"] = np.tile(np.arange(P), len(sym_ids))
+    return recs
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        begin, count = PAR.shard(S, world, rank)
+        local = _all_results(range(begin, begin + count))
+        local_top = D.merge_topk(local, K)
+        top = PAR.gather_topk(local_top, K, dist)
+        tot = PAR.allreduce_counters([count, len(local)], dist)
+        q.put((rank, top.tolist(), tot))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_topk_equals_global(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = D.merge_topk(_all_results(range(S)), K).tolist()
+    for rank, top, tot in out:
+        assert top == expect, rank
+        assert tot == [S, S * len(FAST) * len(SLOW)]
+
+
+def test_shard_covers_every_symbol_once():
+    for n in (1, 7, 5000, 10000):
+        for world in (1, 2, 3, 8):
+            got = []
+            for r in range(world):
+                b, c = PAR.shard(n, world, r)
+                got += list(range(b, b + c))
+            assert got == list(range(n))
