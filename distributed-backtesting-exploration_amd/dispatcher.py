@@ -93,6 +93,9 @@ class Dispatcher:
         with self.files_lock:
             files = split_off_n_jobs(self.files, req.cores)
         if files is None:
+            # main.rs:139-141 answers Status::new(Code::Ok, ...) with no body; grpcio cannot send
+            # an OK status without a message (it surfaces as UNKNOWN), so the empty queue is an
+            # error status here too. Either way the worker ignores it (handlers.rs:59).
             ctx.abort(grpc.StatusCode.NOT_FOUND, "No more jobs available")
         jobs = []
         for path in files:

@@ -1,0 +1,156 @@
+"""BASELINE config 1 end-to-end over the reference's wire contract: a dispatcher counterpart
+serving 16 synthetic daily CSVs and one worker counterpart requesting jobs, processing each
+JobsReply and completing every job with CompleteRequest{id, data}.
+
+CPU test: the worker's processor is the C oracle (test infrastructure standing in for the GPU
+so the control-plane semantics are checked here). GPU test: the processor is libbt.so."""
+import json
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from dbx_amd import dispatcher as DSP
+from dbx_amd import proto as P
+from dbx_amd import worker as WK
+
+N_FILES, BARS = 16, 2520
+
+
+def _write_files(tmp_path):
+    import oracle_np as N
+    paths, closes = [], []
+    o, h, lo, c, v = N.gen(0x5EED, list(range(N_FILES)), BARS, 0)
+    for i in range(N_FILES):
+        pth = tmp_path / f"SYM{i:02d}_daily.csv"
+        pth.write_bytes(N.csv_bytes(o[i], h[i], lo[i], c[i], v[i], 0))
+        paths.append(str(pth))
+        closes.append(c[i].astype(np.int32))
+    return paths, closes
+
+
+def oracle_processor(grid):
+    """Test stand-in for the engine: parse with the C oracle, score every param, format the
+    same JSON lines as the engine (docs/oracle_spec.md §6)."""
+    import orc_ffi as F
+
+    def run(jobs):
+        out = []
+        for _jid, data in jobs:
+            try:
+                _o, _h, _l, c, _v = F.parse_csv(bytes(data))
+            except ValueError as e:
+                out.append(json.dumps({"error": str(e)}) + "\n")
+                continue
+            lines = []
+            for p in range(grid.n_params):
+                kw = grid.param(p)
+                s, _ = F.sma(c, kw["f"], kw["s"], 252)
+                lines.append(json.dumps({"param": p, "n": int(s["n_trades"]), "pnl": int(s["pnl"]),
+                                         "mdd": int(s["mdd"]), "exp": int(s["exposure"]),
+                                         "sharpe": repr(float(s["sharpe"])),
+                                         "h": f"{int(s['hash']):016x}"}))
+            out.append("\n".join(lines) + "\n")
+        return out
+    return run
+
+
+def _run_e2e(tmp_path, processor, grid, cores=4, timeout=60):
+    paths, closes = _write_files(tmp_path)
+    disp = DSP.Dispatcher(paths)
+    replies = []
+    orig = disp.request_jobs
+
+    def spy(req, ctx):  # record which files each reply carried
+        before = list(disp.files)
+        rep = orig(req, ctx)
+        replies.append([p for p in before if p not in disp.files])
+        return rep
+    disp.request_jobs = spy
+    server, port = DSP.serve(disp, "127.0.0.1:0")
+    w = WK.Worker(f"127.0.0.1:{port}", processor, cores=cores, job_tick=0.05, status_tick=0.2)
+    th = threading.Thread(target=w.run, daemon=True)
+    t0 = time.time()
+    th.start()
+    try:
+        while len(disp.jobs_completed) < N_FILES and time.time() - t0 < timeout:
+            time.sleep(0.05)
+    finally:
+        w.stop.set()
+        th.join(10)
+        server.stop(0)
+        disp.close()
+    wall = time.time() - t0
+    assert len(disp.jobs_completed) == N_FILES, f"completed {len(disp.jobs_completed)}"
+    return disp, replies, paths, closes, wall
+
+
+def _check_results(disp, paths, closes, grid):
+    import orc_ffi as F
+    by_path = {disp.job_paths[j]: d for j, d in disp.results.items()}
+    for pth, c in zip(paths, closes):
+        lines = by_path[pth].strip().split("\n")
+        assert len(lines) == grid.n_params
+        for p, line in enumerate(lines):
+            j = json.loads(line)
+            kw = grid.param(p)
+            s, _ = F.sma(c, kw["f"], kw["s"], 252)
+            assert j["param"] == p and j["n"] == int(s["n_trades"]) and j["pnl"] == int(s["pnl"])
+            assert j["mdd"] == int(s["mdd"]) and float(j["sharpe"]) == float(s["sharpe"])
+            assert int(j["h"], 16) == int(s["hash"])
+
+
+def test_config1_end_to_end_cpu_processor(tmp_path):
+    grid = D.config2_grid()
+    disp, replies, paths, closes, wall = _run_e2e(tmp_path, oracle_processor(grid), grid)
+    # split_off semantics (server/main.rs:151-162): reply 1 = files[4..16], reply 2 = files[0..4]
+    nonempty = [r for r in replies if r]
+    assert nonempty[0] == paths[4:] and nonempty[1] == paths[:4]
+    _check_results(disp, paths, closes, grid)
+
+
+@pytest.mark.gpu
+def test_config1_end_to_end_gpu_engine(tmp_path):
+    grid = D.config2_grid()
+    with D.Engine(grid) as eng:
+        disp, replies, paths, closes, wall = _run_e2e(tmp_path, WK.engine_processor(eng), grid)
+    _check_results(disp, paths, closes, grid)
+    print(f"config 1 end-to-end: {N_FILES} jobs in {wall:.2f} s wall")
+
+
+def test_split_off_semantics():
+    f = list("abcdefghijklmnop")
+    assert DSP.split_off_n_jobs(f, 4) == list("efghijklmnop") and f == list("abcd")
+    assert DSP.split_off_n_jobs(f, 4) == list("abcd") and f == []
+    assert DSP.split_off_n_jobs(f, 4) is None
+    g = list("xyz")
+    assert DSP.split_off_n_jobs(g, 0) == list("xyz") and g == []
+
+
+def test_wire_bytes_match_reference_contract(golden_dir):
+    pins = json.load(open(os.path.join(golden_dir, "wire.json")))
+    assert P.JobsRequest(cores=4).SerializeToString().hex() == pins["JobsRequest{cores=4}"]
+    assert P.StatusRequest(status=P.RUNNING).SerializeToString().hex() == pins["StatusRequest{RUNNING}"]
+    rep = P.JobsReply(jobs=[P.Job(id="abc", File=b"t,o,h,l,c,v\n")])
+    assert rep.SerializeToString().hex() == pins["JobsReply{[Job{id:'abc', File:'t,o,h,l,c,v\\n'}]}"]
+    # field numbers/types of the other messages (proto:29-32)
+    cr = P.CompleteRequest(id="i", data="d").SerializeToString()
+    assert cr == b"\x0a\x01i\x12\x01d"
+
+
+def test_process_incoming_job_flag_and_order():
+    import queue
+    seen = []
+
+    def proc(jobs):
+        assert WK.PROC_FLAG.is_set()       # process.rs:18
+        seen.extend(j for j, _ in jobs)
+        return [f"r{j}" for j, _ in jobs]
+    q = queue.Queue()
+    rep = P.JobsReply(jobs=[P.Job(id=str(i), File=b"x") for i in range(5)])
+    WK.process_incoming_job(rep, q, proc)
+    assert not WK.PROC_FLAG.is_set()       # process.rs:28
+    assert [q.get_nowait() for _ in range(5)] == [(str(i), f"r{i}") for i in range(5)]
