@@ -10,12 +10,15 @@
 //            of doubles (exact below 2^53); fixed-point returns q, q2 (spec §3) and their
 //            in-tile int64 prefixes + int128 tile base; the tile's disjoint sparse table (DST) of
 //            the close path (max, min, drawdown, draw-up), built by log-doubling shuffles.
-//   stage 2, tile k+1 (all waves): int32 SMA keys K[w][b] = floor(window_sum / w) for every
-//            window of the grid (one f64 multiply + exact fix-up, no division).
-//   stage 3, tile k (all waves, lane = (fast, slow) pair): 2 integer compares per bar give two
-//            64-bit words G (fast key > slow key) and L (<). Keys are monotone in the exact SMA,
-//            so a strict key order is the exact order; equal keys (rare) are settled exactly
-//            (F*s vs L*f in f64, products < 2^53). The whole tile's position path then follows
+//   stage 2, tile k+1 (all waves, helper included; lane = bar, window wave-uniform): int32 SMA
+//            keys K[w][b] = floor(window_sum / w) for every window of the grid (one f64
+//            multiply + exact fix-up, no division).
+//   stage 3, tile k (parameter waves, lane = (fast, slow) pair): per bar one subtract whose
+//            sign bit is shifted into the 64-bit word L (fast key < slow key), and a running
+//            unsigned min that detects equal keys; without equal keys G (fast > slow) = ~L.
+//            Keys are monotone in the exact SMA, so a strict key order is the exact order; equal
+//            keys (rare: ~1e-4 of lane-tiles on config 2) are settled exactly (F*s vs L*f in
+//            f64, products < 2^53). The whole tile's position path then follows
 //            bit-parallel: a set/reset latch is an add-with-carry (LONG = carries of
 //            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
 //            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
@@ -31,7 +34,7 @@ constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned
 constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
 
 struct SmaLds {                       // byte offsets into dynamic LDS
-    size_t ring, keys, invw, win, dst, ct, ql, total;
+    size_t ring, keys, invw, win, dst, ct, ql, ctr, total;
 };
 
 __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
@@ -45,6 +48,7 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
+    L.ctr = take(4);
     L.total = o;
     return L;
 }
@@ -61,12 +65,16 @@ struct ScanCarry {
     int32_t prevc;      // close of the bar before the tile
 };
 
-__device__ __forceinline__ void stage_scan(const int32_t* __restrict__ crow, int B, int t0, int lane,
-                                           int R, double* ring, int32_t* cT, int64_t* ql, Agg* D,
-                                           ScanCarry& cy) {
+__device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, int B, int t) {
+    return t < B ? crow[t] : 0;
+}
+
+// c = close of bar t0 + lane (0 past the end), loaded one tile ahead by the caller so the HBM
+// latency is off the pipeline's critical path.
+__device__ __forceinline__ void stage_scan(int32_t c, int B, int t0, int lane, int R, double* ring,
+                                           int32_t* cT, int64_t* ql, Agg* D, ScanCarry& cy) {
     const int t = t0 + lane;
     const bool valid = t < B;
-    const int32_t c = valid ? crow[t] : 0;
     // previous bar's close: DPP wave_shr:1, lane 0 takes the carry
     const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
                                                             0x138, 0xf, 0xf, false);
@@ -98,54 +106,67 @@ __device__ __forceinline__ void stage_scan(const int32_t* __restrict__ crow, int
     }
 }
 
-// Stage 2 for one tile: int32 floor keys for every window (all threads of the block).
-__device__ __forceinline__ void stage_keys(int t0, int B, int nw, int R, const double* ring,
+// Stage 2 for one tile: int32 floor keys for every window. lane = bar, so the window length
+// and its reciprocal are wave-uniform and the top of the ring is read once per tile.
+// Windows are handed out dynamically: every wave of the block (helper included) grabs window
+// indices from an LDS counter after its other work for the tile, so waves with few flips to
+// walk compute more keys. Round r owns counter values [r*(nw+nwaves), (r+1)*(nw+nwaves)):
+// nw successful grabs plus exactly one failing grab per wave (the barrier separates rounds).
+// Bars without a full window (or past the series end) get key -1 on fast rows and -2 on slow
+// rows: their difference is never 0, so they never look like ties to the compare stage (they
+// are outside every lane's decision mask anyway).
+__device__ __forceinline__ uint32_t grab(uint32_t* ctr, int lane) {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(ctr, 1u);
+    return __builtin_amdgcn_readlane(v, 0);
+}
+
+__device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R, const double* ring,
                                            const int32_t* win, const double* invw, int32_t* K,
-                                           int tid, int nthreads) {
-    for (int idx = tid; idx < nw * kTile; idx += nthreads) {
-        const int w = idx >> 6, b = idx & 63;
-        const int t = t0 + b;
-        const int W = win[w];
-        int32_t key = 0;
-        if (t < B && t + 1 - W >= 0) {
-            const double F = ring[(t + 1) & (R - 1)] - ring[(t + 1 - W) & (R - 1)];  // exact
-            double fl = floor(F * invw[w]);                  // within 1 of floor(F / W)
-            const double r = F - fl * (double)W;             // exact (all terms < 2^53)
-            fl += r < 0.0 ? -1.0 : (r >= (double)W ? 1.0 : 0.0);
-            key = (int32_t)fl;
-        }
-        K[w * kKS + b] = key;
+                                           uint32_t* ctr, uint32_t round, int nwaves, int lane) {
+    const int t = t0 + lane;
+    const double top = ring[(t + 1) & (R - 1)];
+    const bool tin = t < B;
+    const uint32_t base = round * (uint32_t)(nw + nwaves);
+    uint32_t w = grab(ctr, lane) - base;
+#pragma unroll 1
+    while (w < (uint32_t)nw) {
+        const uint32_t nxt = grab(ctr, lane) - base;  // in flight while this window computes
+        const int W = __builtin_amdgcn_readfirstlane(win[w]);
+        const double iw = invw[w];
+        const double F = top - ring[(t + 1 - W) & (R - 1)];  // exact (< 2^53)
+        const double fl = floor(F * iw);                       // within 1 of floor(F / W)
+        const double r = F - fl * (double)W;                   // exact
+        int32_t key = (int32_t)fl;
+        key -= (int32_t)(r < 0.0);
+        key += (int32_t)(r >= (double)W);
+        const bool valid = tin && t + 1 - W >= 0;
+        K[w * kKS + lane] = valid ? key : ((int)w < nf ? -1 : -2);
+        w = nxt;
     }
 }
 
-// Four bars: G = 2G + [x > y], L = 2L + [x < y] per bar. v_cmp writes a lane mask to an SGPR
-// pair and v_addc consumes it as carry-in: 2 VALU per compare instead of cmp+cndmask+shift-or.
-// Masks rotate over four SGPR pairs so each is read >= 2 instructions after its write
-// (gfx950: VALU write of an SGPR -> VALU read as carry needs 2 wait states).
-__device__ __forceinline__ void cmp4(uint32_t& g, uint32_t& l, const int4& x, const int4& y) {
-    uint64_t m0, m1, m2, m3, co;
-    asm volatile(
-        "v_cmp_gt_i32_e64 %[m0], %[x0], %[y0]\n\t"
-        "v_cmp_lt_i32_e64 %[m1], %[x0], %[y0]\n\t"
-        "v_cmp_gt_i32_e64 %[m2], %[x1], %[y1]\n\t"
-        "v_cmp_lt_i32_e64 %[m3], %[x1], %[y1]\n\t"
-        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m0]\n\t"
-        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m1]\n\t"
-        "v_cmp_gt_i32_e64 %[m0], %[x2], %[y2]\n\t"
-        "v_cmp_lt_i32_e64 %[m1], %[x2], %[y2]\n\t"
-        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m2]\n\t"
-        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m3]\n\t"
-        "v_cmp_gt_i32_e64 %[m2], %[x3], %[y3]\n\t"
-        "v_cmp_lt_i32_e64 %[m3], %[x3], %[y3]\n\t"
-        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m0]\n\t"
-        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m1]\n\t"
-        "s_nop 0\n\t"
-        "v_addc_co_u32_e64 %[g], %[co], %[g], %[g], %[m2]\n\t"
-        "v_addc_co_u32_e64 %[l], %[co], %[l], %[l], %[m3]"
-        : [g] "+v"(g), [l] "+v"(l), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
-          [m3] "=&s"(m3), [co] "=&s"(co)
-        : [x0] "v"(x.x), [y0] "v"(y.x), [x1] "v"(x.y), [y1] "v"(y.y), [x2] "v"(x.z),
-          [y2] "v"(y.z), [x3] "v"(x.w), [y3] "v"(y.w));
+// Four bars, 10 VALU: d = x - y (no overflow: keys are in [-2, 2^31)); the sign bit of d is
+// [x < y] and is shifted into L by v_alignbit ({l, d} >> 31 == l << 1 | d >> 31); z keeps the
+// unsigned minimum of every d, which is 0 iff some bar has equal keys. With no equal keys,
+// [x > y] is simply ~[x < y]; a tile with an equal pair takes the exact path.
+__device__ __forceinline__ void cmp4(uint32_t& l, uint32_t& z, const int4& x, const int4& y) {
+    const uint32_t d0 = (uint32_t)(x.x - y.x), d1 = (uint32_t)(x.y - y.y);
+    const uint32_t d2 = (uint32_t)(x.z - y.z), d3 = (uint32_t)(x.w - y.w);
+    l = __builtin_amdgcn_alignbit(l, d0, 31);
+    l = __builtin_amdgcn_alignbit(l, d1, 31);
+    l = __builtin_amdgcn_alignbit(l, d2, 31);
+    l = __builtin_amdgcn_alignbit(l, d3, 31);
+    z = min(z, min(d0, d1));
+    z = min(z, min(d2, d3));
+}
+
+// Equality word for the rare tiles with equal keys (same bit order as cmp4).
+__device__ __forceinline__ uint64_t eq_word(const int32_t* k1, const int32_t* k2) {
+    uint64_t e = 0;
+#pragma unroll 1
+    for (int b = 0; b < kTile; ++b) e |= (uint64_t)(k1[b] == k2[b]) << b;
+    return e;
 }
 
 }  // namespace
@@ -229,12 +250,14 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     // the last wave is a dedicated helper: stage 1 only, no parameter lanes
     const int nparam_threads = (int)blockDim.x - 64;
     const bool helper = tid >= nparam_threads;
+    const int nwaves = (int)blockDim.x >> 6;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
     const int ntiles = (B + kTile - 1) / kTile;
@@ -250,19 +273,30 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
         win[w] = W;
         invw[w] = 1.0 / (double)W;
     }
-    if (tid == 0) ring[0] = 0.0;
+    if (tid == 0) {
+        ring[0] = 0.0;
+        *ctr = 0;
+    }
     __syncthreads();
     const int fw = win[kf], sw = win[ks];
     const int warm = (fw > sw ? fw : sw) - 1;  // first decision bar of this lane
 
     ScanCarry cy{0, 0};
-    // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0
-    if (helper) stage_scan(crow, B, 0, lane, R, ring, cts, qls, dst, cy);
-    __syncthreads();
-    if (helper && ntiles > 1)
-        stage_scan(crow, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile,
-                   dst + kDstLevels * kTile, cy);
-    if (!helper) stage_keys(0, B, nw, R, ring, win, invw, keys, tid, nparam_threads);
+    // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0. The helper keeps the closes of the
+    // tile after next in flight (cpre) across the barrier.
+    int32_t cpre = 0;
+    if (helper) {
+        const int32_t c0 = load_close(crow, B, lane), c1 = load_close(crow, B, kTile + lane);
+        cpre = load_close(crow, B, 2 * kTile + lane);
+        stage_scan(c0, B, 0, lane, R, ring, cts, qls, dst, cy);
+        __syncthreads();
+        if (ntiles > 1)
+            stage_scan(c1, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile,
+                       dst + kDstLevels * kTile, cy);
+    } else {
+        __syncthreads();
+    }
+    stage_keys(0, B, nw, nf, R, ring, win, invw, keys, ctr, 0, nwaves, lane);
     __syncthreads();
 
     SmaAcct a;
@@ -291,17 +325,15 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
 
     for (int k = 0; k < ntiles; ++k) {
         const int t0 = k * kTile;
-        // ---- stage 1 (tile k+2) and stage 2 (tile k+1): independent of stage 3 (tile k)
+        // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
+        // (tile k+1) on every wave, balanced dynamically
         if (helper && k + 2 < ntiles && !(g.ablate & 1)) {
             const int s = (k + 2) % kStages;
-            stage_scan(crow, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+            stage_scan(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
                        qls + s * 2 * kTile, dst + s * kDstLevels * kTile, cy);
+            cpre = load_close(crow, B, t0 + 3 * kTile + lane);
         }
         BT_STAMP(0)
-        if (!helper && k + 1 < ntiles && !(g.ablate & 2))
-            stage_keys(t0 + kTile, B, nw, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
-                       tid, nparam_threads);
-        BT_STAMP(1)
         // ---- stage 3 (tile k)
         if (active) {
             const int s = k % kStages;
@@ -311,27 +343,32 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             const int32_t* K = keys + (k & 1) * nw * kKS;
             const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
             const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
-            uint32_t g0 = 0, l0 = 0, g1 = 0, l1 = 0;
+            uint32_t l0 = 0, l1 = 0, z = ~0u;
 #pragma unroll 1
-            for (int v0 = 0; v0 < 8 && !(g.ablate & 4); v0 += 4) {
+            for (int v0 = 0; v0 < 8 && !(g.ablate & 4); v0 += 2) {
 #pragma unroll
-                for (int v = v0; v < v0 + 4; ++v) cmp4(g0, l0, k1[v], k2[v]);
+                for (int v = v0; v < v0 + 2; ++v) cmp4(l0, z, k1[v], k2[v]);
             }
 #pragma unroll 1
-            for (int v0 = 8; v0 < 16 && !(g.ablate & 4); v0 += 4) {
+            for (int v0 = 8; v0 < 16 && !(g.ablate & 4); v0 += 2) {
 #pragma unroll
-                for (int v = v0; v < v0 + 4; ++v) cmp4(g1, l1, k1[v], k2[v]);
+                for (int v = v0; v < v0 + 2; ++v) cmp4(l1, z, k1[v], k2[v]);
             }
             BT_STAMP(2)
-            uint64_t G = ((uint64_t)__builtin_bitreverse32(g1) << 32) | __builtin_bitreverse32(g0);
             uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
             const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
             uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
             const int wb = warm - t0;
             vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
-            G &= vm;
+            uint64_t G, T = 0;
+            if (z != 0) {
+                G = ~L & vm;
+            } else {  // some bar has equal floor keys: settle those exactly
+                const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
+                G = ~(L | E) & vm;
+                T = E & vm;
+            }
             L &= vm;
-            uint64_t T = ~(G | L) & vm;  // equal floor keys: settle exactly
             while (T) {
                 const int b = __builtin_ctzll(T);
                 T &= T - 1;
@@ -394,6 +431,10 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
             a.ps1 = a.ps2 = 0;
             BT_STAMP(5)
         }
+        if (k + 1 < ntiles && !(g.ablate & 2))
+            stage_keys(t0 + kTile, B, nw, nf, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
+                       ctr, (uint32_t)(k + 1), nwaves, lane);
+        BT_STAMP(1)
         __syncthreads();
         BT_STAMP(6)
     }
