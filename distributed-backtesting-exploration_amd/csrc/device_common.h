@@ -14,7 +14,7 @@ typedef __int128 i128;
 // Price-path aggregate over a run of closes, in order: max, min, max drawdown (max over
 // i<=j of c_i - c_j), max draw-up (max over i<=j of c_j - c_i). Prices < 2^31, so every
 // field fits int32.
-struct Agg {
+struct __attribute__((aligned(16))) Agg {
     int32_t mx, mn, dd, du;
 };
 
