@@ -81,7 +81,6 @@ struct bt_engine {
     int64_t rows = 0;
     DevBuf<SymDesc> d_syms;
     DevBuf<int32_t> d_c, d_h, d_l;
-    DevBuf<int64_t> d_q, d_q2;
     // outputs
     DevBuf<bt_summary> d_sum;
     DevBuf<uint64_t> d_key;
@@ -109,8 +108,8 @@ bool has_hl(const bt_engine* e) { return e->cfg.strategy == BT_BOLL; }
 const char* kernel_name(int32_t strategy) {
     switch (strategy) {
         case BT_SMA_CROSS: return "bt::sma_kernel";
-        case BT_EMA_OLS: return "bt::ema_ols_kernel";
-        default: return "bt::boll_kernel";
+        case BT_EMA_OLS: return "bt::ema_tile_kernel";
+        default: return "bt::boll_tile_kernel";
     }
 }
 
@@ -148,10 +147,14 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             if (!(err = copy_axis(0, c.span, c.n_span, "span", 1, kMaxBars)).empty()) return err;
             if (!(err = copy_axis(1, c.ols, c.n_ols, "ols", 1, 1 << 16)).empty()) return err;
             if (c.band_bps < 0 || c.band_bps >= 10000) return "band_bps out of range";
+            if (c.n_span > 64) return "EMA grid: at most 64 spans (one helper lane per span)";
             e->grid.na = c.n_span;
             e->grid.nb = c.n_ols;
             e->grid.nc = e->grid.nd = 1;
             e->grid.band_bps = c.band_bps;
+            e->grid.wmax = *std::max_element(e->ax[1].begin(), e->ax[1].end());
+            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
+            if (ema_lds_bytes(e->grid) > 160 * 1024) return "EMA grid needs more LDS than a CU has (OLS windows too long)";
             break;
         }
         case BT_BOLL: {
@@ -165,6 +168,9 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             e->grid.nc = c.n_sl;
             e->grid.nd = c.n_tp;
             e->grid.k_den = c.k_den;
+            e->grid.wmax = *std::max_element(e->ax[0].begin(), e->ax[0].end());
+            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
+            if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;
         }
         default:
@@ -212,10 +218,6 @@ void layout(bt_engine* e, int32_t n_sym, const int32_t* bars, const int64_t* ids
     if (has_hl(e)) {
         e->d_h.ensure(rows);
         e->d_l.ensure(rows);
-    }
-    if (e->cfg.strategy != BT_SMA_CROSS) {
-        e->d_q.ensure(rows);
-        e->d_q2.ensure(rows);
     }
     e->ran = false;
 }
@@ -277,12 +279,11 @@ void run_impl(bt_engine* e) {
             err = launch_sma(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
             break;
         case BT_EMA_OLS:
-            err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->d_q.p, e->d_q2.p, e->grid, out, parity,
-                                 e->stream);
+            err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
             break;
         case BT_BOLL:
-            err = launch_boll(e->d_syms.p, S, e->d_h.p, e->d_l.p, e->d_c.p, e->d_q.p, e->d_q2.p,
-                              e->grid, out, parity, e->stream);
+            err = launch_boll(e->d_syms.p, S, e->d_h.p, e->d_l.p, e->d_c.p, e->grid, out, parity,
+                              e->stream);
             break;
     }
     HIPCHK(err);
@@ -465,8 +466,6 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_c.release();
         e->d_h.release();
         e->d_l.release();
-        e->d_q.release();
-        e->d_q2.release();
         e->d_sum.release();
         e->d_key.release();
         e->d_sums.release();

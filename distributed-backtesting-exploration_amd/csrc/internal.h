@@ -24,8 +24,8 @@ struct Grid {
     int32_t n_params;
     int32_t na, nb, nc, nd;        // axis sizes (SMA: fast, slow; EMA: span, ols; BOLL: w,k,sl,tp)
     int32_t band_bps, k_den;
-    int32_t wmax;                  // largest window of the grid (SMA ring sizing)
-    int32_t ring;                  // SMA prefix ring length (power of two >= wmax + kTile)
+    int32_t wmax;                  // largest window of the grid (prefix ring sizing)
+    int32_t ring;                  // prefix ring length (power of two >= wmax + 3 kTile)
     double sqrt_ann;               // sqrt((double)annualization), computed on the host
     int32_t ablate;                // profiling only (env BT_ABLATE): phases to skip, 0 = none
     const int32_t* a;              // device arrays
@@ -51,13 +51,13 @@ hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t
 size_t sma_lds_bytes(const Grid& g);  // dynamic LDS of the SMA kernel for this grid
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                       const Out& out, bool parity, hipStream_t st);
-// q/q2: [rows] int64 scratch for the fixed-point returns (spec §3) of every bar.
-hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close,
-                          int64_t* q, int64_t* q2, const Grid& g, const Out& out, bool parity,
-                          hipStream_t st);
-hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high,
-                       const int32_t* low, const int32_t* close, int64_t* q, int64_t* q2,
-                       const Grid& g, const Out& out, bool parity, hipStream_t st);
+size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
+size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
+hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                          const Out& out, bool parity, hipStream_t st);
+hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, const int32_t* low,
+                       const int32_t* close, const Grid& g, const Out& out, bool parity,
+                       hipStream_t st);
 
 // Top-k by radix select over `key` (k_topk.hip): device-side finish into `out`.
 constexpr int kTopkCap = 2048;      // candidates sorted in LDS by the finish kernel

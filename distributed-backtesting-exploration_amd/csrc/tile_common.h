@@ -1,0 +1,160 @@
+// tile_common.h — pieces shared by the tile-pipelined strategy kernels (k_tile.hip):
+// the per-tile close scan (returns, drawdown sparse table) and the per-lane trade accounting
+// that runs only at position changes. Spec: docs/oracle_spec.md §3-§4.
+#pragma once
+#include "device_common.h"
+
+namespace bt {
+
+constexpr int kTileStages = 3;  // tile buffers in flight: scanned (k+2), flagged (k+1), walked (k)
+
+// Wave-wide shuffle of an Agg from lane `src`.
+__device__ __forceinline__ Agg tile_shfl_agg(const Agg& a, int src) {
+    return Agg{__shfl(a.mx, src, 64), __shfl(a.mn, src, 64), __shfl(a.dd, src, 64),
+               __shfl(a.du, src, 64)};
+}
+
+struct TileCarry {
+    int64_t P;       // sum of closes before the tile
+    int32_t prevc;   // close of the bar before the tile
+};
+
+// One whole wave, lane = bar t0 + lane, c = its close (0 past the end): writes the tile's
+// closes cT[64], the in-tile prefixes of the fixed-point returns ql[0..63] (q) and
+// ql[64..127] (q2), and the disjoint sparse table D[6][64] of the close path. Returns the
+// inclusive prefix sum of closes up to this lane's bar (exact int64).
+__device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane, int32_t* cT,
+                                             int64_t* ql, Agg* D, TileCarry& cy) {
+    const int t = t0 + lane;
+    const bool valid = t < B;
+    const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
+                                                            0x138, 0xf, 0xf, false);  // wave_shr:1
+    const int64_t inc = wave_iscan_i64((int64_t)c);
+    const int64_t pre = cy.P + inc;
+    cT[lane] = c;
+    int64_t q = 0, q2 = 0;
+    if (valid && t >= 1) fixed_ret(c, cp, q, q2);
+    ql[lane] = wave_iscan_i64(q);
+    ql[kTile + lane] = wave_iscan_i64(q2);
+    cy.P += lane63_i64(inc);
+    cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
+    Agg S = agg_one(c), Pp = S;
+    D[lane] = S;
+#pragma unroll
+    for (int m = 1; m < kDstLevels; ++m) {
+        const int half = 1 << (m - 1);
+        const bool left = (lane & half) == 0;
+        const Agg expose = agg_sel(left, S, Pp);
+        const int src = left ? (lane | (2 * half - 1)) : (lane & ~(2 * half - 1));
+        const Agg part = tile_shfl_agg(expose, src);
+        S = agg_sel(left, agg_merge(S, part), S);
+        Pp = agg_sel(left, Pp, agg_merge(part, Pp));
+        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
+    }
+    return pre;
+}
+
+// Per-lane trade accounting (spec §4), touched only when the position changes.
+//  * drawdown via gap = peak - realized (int64 >= 0): a closed trade whose MTM path has range
+//    [lo, hi] and internal drawdown `path` gives mdd = max(mdd, gap - lo, path) and
+//    gap' = max(gap, hi) - pnl;
+//  * S1/S2 via per-tile partial sums of the in-tile return prefixes QL (uint64, exact modulo
+//    2^64, folded into int128 at the tile end): a position change at bar b from pos to np adds
+//    (pos - np) * QL[b] to ps1 and (|pos| - |np|) * QL2[b] to ps2; an open position at the tile
+//    end adds pos * QL[63] and QL2[63].
+struct TradeAcct {
+    int32_t pos, e, ce, sb, ntr, expo;  // sb: in-tile bar where the open trade's path resumes
+    int64_t R, gap, mdd;
+    uint64_t ps1, ps2, h;
+    i128 s1, s2;
+    Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
+};
+
+__device__ __forceinline__ void acct_init(TradeAcct& a) {
+    a.pos = a.e = a.ce = a.sb = a.ntr = a.expo = 0;
+    a.R = a.gap = a.mdd = 0;
+    a.ps1 = a.ps2 = 0;
+    a.h = kFnvOff;
+    a.s1 = a.s2 = 0;
+    a.agg = kAggId;
+}
+
+// Close the open trade at global bar t for price px; `st` aggregates the trade's whole price
+// path in order, exit point included.
+template <bool PARITY>
+__device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
+                                           bt_trade* tr, int cap) {
+    const bool lg = a.pos > 0;
+    const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;  // |.| < 2^31
+    const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
+    const int32_t path = lg ? st.dd : st.du;
+    const int32_t pnl = lg ? px - a.ce : a.ce - px;
+    a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+    a.gap = max(a.gap, (int64_t)hi) - pnl;
+    a.R += pnl;
+    a.expo += t - a.e;
+    const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
+                       ((uint64_t)lg << 62);
+    a.h = (a.h ^ w) * kFnvPrime;
+    if (PARITY && a.ntr < cap) {
+        bt_trade r;
+        r.entry_bar = a.e;
+        r.exit_bar = t;
+        r.side = a.pos;
+        r.pad = 0;
+        r.entry_px = a.ce;
+        r.exit_px = px;
+        tr[a.ntr] = r;
+    }
+    a.ntr++;
+}
+
+__device__ __forceinline__ void acct_open(TradeAcct& a, int t, int b, int32_t px) {
+    a.e = t;
+    a.ce = px;
+    a.sb = b;
+    a.agg = kAggId;
+}
+
+// Tile end: carry the open trade's path, fold the tile's return partials into int128.
+__device__ __forceinline__ void acct_tile_end(TradeAcct& a, const Agg* D, const int64_t* ql) {
+    if (a.pos != 0) {
+        a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
+        a.sb = 0;
+        const uint64_t q63 = (uint64_t)ql[kTile - 1];
+        a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
+        a.ps2 += (uint64_t)ql[2 * kTile - 1];
+    }
+    a.s1 += (i128)(int64_t)a.ps1;
+    a.s2 += (i128)(int64_t)a.ps2;
+    a.ps1 = a.ps2 = 0;
+}
+
+__device__ __forceinline__ void acct_write(const TradeAcct& a, int bars, double sqrt_ann,
+                                           size_t gi, const Out& out) {
+    const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
+    const int64_t s1hi = (int64_t)(a.s1 >> 64), s2hi = (int64_t)(a.s2 >> 64);
+    const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, bars, sqrt_ann);
+    bt_summary r;
+    r.n_trades = a.ntr;
+    r.status = 0;
+    r.pnl = a.R;
+    r.mdd = a.mdd;
+    r.exposure = a.expo;
+    r.sharpe = sh;
+    r.hash = a.h;
+    out.sum[gi] = r;
+    out.key[gi] = order_key(sh);
+    if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
+}
+
+// Decision-bar mask of a tile: bits for bars t0+b with lo <= t0+b <= hi.
+__device__ __forceinline__ uint64_t bar_range_mask(int t0, int lo, int hi) {
+    const int a = lo - t0, b = hi - t0;
+    if (b < 0 || a > 63 || a > b) return 0;
+    const uint64_t top = b >= 63 ? ~0ULL : ((1ULL << (b + 1)) - 1);
+    const uint64_t bot = a <= 0 ? ~0ULL : (~0ULL << a);
+    return top & bot;
+}
+
+}  // namespace bt

@@ -185,3 +185,66 @@ def test_topk_massive_ties_host_finish():
         top = e.read_topk()
     assert [(int(t["sym"]), int(t["param"])) for t in top] == [(1000 + i // 9, i % 9) for i in range(50)]
     assert all(float(t["sharpe"]) == 0.0 for t in top)
+
+
+TILE_GRIDS = {
+    "ema_ols": lambda: D.Grid.ema_ols([2, 3, 10, 100], [2, 4, 70, 200], band_bps=20),
+    "boll": lambda: D.Grid.boll([2, 3, 20, 70, 130], [1, 4], [50, 100], [50, 400], k_den=2),
+}
+
+
+@pytest.mark.parametrize("bars", [1, 2, 63, 64, 65, 130, 1000])
+@pytest.mark.parametrize("strategy", ["ema_ols", "boll"])
+def test_tile_strategies_ragged(strategy, bars):
+    """Tile kernels on every tile-boundary case, windows shorter and longer than a tile."""
+    grid = TILE_GRIDS[strategy]()
+    o, h, lo, c = _gen(0x5EED, [5, 6], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 5, 2, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(2):
+        orc, otr = oracle_row(strategy, grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} bars {bars} sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.parametrize("strategy", ["ema_ols", "boll"])
+def test_tile_strategies_edges(strategy, golden_dir):
+    """Golden edge series (flat, near 2^31 ticks, saw-tooth, 1-2 tick moves, 1-2 bars) with
+    their own highs and lows, loaded as ragged rows in one batch."""
+    import json, os
+    edge = json.load(open(os.path.join(golden_dir, "edge.json")))
+    cols = [[np.array(x[k], np.int32) for x in edge] for k in ("c", "h", "l")]
+    grid = TILE_GRIDS[strategy]()
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_ohlc(cols[0], cols[1], cols[2])
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, x in enumerate(edge):
+        orc, otr = oracle_row(strategy, grid, (cols[0][s], cols[1][s], cols[2][s], cols[0][s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} {x['name']} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.parametrize("config", [3, 4])
+def test_config34_grids_long_series(config):
+    """BASELINE config 3 / 4 grids (all 64 / 256 params) on 1-min series of 20,000 bars."""
+    grid = D.config3_grid() if config == 3 else D.config4_grid()
+    strategy = "ema_ols" if config == 3 else "boll"
+    bars, syms = 20000, [0, 1]
+    o, h, lo, c = _gen(0x5EED, syms, bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 0, len(syms), bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(len(syms)):
+        orc, otr = oracle_row(strategy, grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"config {config} sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
