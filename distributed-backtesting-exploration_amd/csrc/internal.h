@@ -9,7 +9,6 @@ namespace bt {
 
 constexpr int kTile = 64;          // bars per LDS tile (one bit per bar in a 64-bit word)
 constexpr int kRowAlign = 64;      // symbol rows start on 64-element boundaries in HBM
-constexpr int kMaxBlock = 512;     // threads per workgroup (8 waves)
 
 // One symbol of the HBM-resident dataset: rows of int32 ticks at `off` in every column.
 struct SymDesc {
@@ -49,6 +48,12 @@ struct Out {
 hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
                       int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st);
 size_t sma_lds_bytes(const Grid& g);  // dynamic LDS of the SMA kernel for this grid
+struct SmaShape {                     // SMA launch shape for P parameters (k_sma.hip)
+    int pw;                           // parameter waves per block
+    int dedicated;                    // 1: an extra helper wave runs the tile scan
+    int block, gy;                    // threads per block, y-blocks per symbol
+};
+SmaShape sma_shape(int P);
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                       const Out& out, bool parity, hipStream_t st);
 size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel

@@ -240,9 +240,9 @@ __device__ __forceinline__ void sma_flip(SmaAcct& a, int b, int t0, int bl, uint
 }
 
 template <bool PARITY, bool STAMPS>
-__global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restrict__ syms,
-                                                        const int32_t* __restrict__ close,
-                                                        Grid g, Out out) {
+__global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ syms,
+                                                   const int32_t* __restrict__ close, Grid g,
+                                                   Out out, int dedicated) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nf = g.na, ns = g.nb, nw = nf + ns;
     const int R = g.ring;
@@ -258,10 +258,11 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    // the last wave is a dedicated helper: stage 1 only, no parameter lanes
-    const int nparam_threads = (int)blockDim.x - 64;
-    const bool helper = tid >= nparam_threads;
+    // the last wave runs stage 1; with `dedicated` it is a helper with no parameter lanes,
+    // otherwise (a grid that fills all 16 waves of one block) it also walks 64 parameters
     const int nwaves = (int)blockDim.x >> 6;
+    const bool helper = (tid >> 6) == nwaves - 1;
+    const int nparam_threads = dedicated ? (int)blockDim.x - 64 : (int)blockDim.x;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
     const int ntiles = (B + kTile - 1) / kTile;
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
     // loop (a wave iterates max-over-lanes flips) wastes fewer lanes (config 2: 2.51 -> 2.11
     // iterations per wave-tile). Results stay in param order p = fast * ns + slow.
     const int j = blockIdx.y * nparam_threads + tid;
-    const bool active = !helper && j < P;
+    const bool active = tid < nparam_threads && j < P;
     const int kf = active ? j % nf : 0;
     const int ks = nf + (active ? j / nf : 0);
     const int p = (kf * ns) + (ks - nf);
@@ -474,21 +475,37 @@ __global__ __launch_bounds__(kMaxBlock) void sma_kernel(const SymDesc* __restric
 
 size_t sma_lds_bytes(const Grid& g) { return sma_lds_layout(g.ring, g.na + g.nb).total; }
 
+// Block shape: one block per symbol when the parameters fit (<= 15 parameter waves + a helper,
+// or exactly 16 waves with the scan folded into the last parameter wave), otherwise the fewest
+// equal y-blocks; each y-block recomputes the tile scan and keys, so splits are avoided.
+SmaShape sma_shape(int P) {
+    const int need = (P + 63) / 64;
+    SmaShape s;
+    if (need == 16) {
+        s.pw = 16;
+        s.dedicated = 0;
+    } else {
+        const int nby = (need + 14) / 15;
+        s.pw = (need + nby - 1) / nby;
+        s.dedicated = 1;
+    }
+    s.block = 64 * (s.pw + s.dedicated);
+    s.gy = (P + 64 * s.pw - 1) / (64 * s.pw);
+    return s;
+}
+
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                       const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int P = g.n_params;
-    // parameter waves (<= 7) plus one helper wave per workgroup
-    const int pw = std::min((P + 63) / 64, kMaxBlock / 64 - 1);
-    const int block = 64 * (pw + 1);
-    const dim3 grid(n_sym, (P + 64 * pw - 1) / (64 * pw));
+    const SmaShape sh = sma_shape(g.n_params);
+    const dim3 grid(n_sym, sh.gy), block(sh.block);
     const size_t lds = sma_lds_bytes(g);
     if (g.ablate & 64)
-        hipLaunchKernelGGL((sma_kernel<false, true>), grid, dim3(block), lds, st, syms, close, g, out);
+        hipLaunchKernelGGL((sma_kernel<false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity)
-        hipLaunchKernelGGL((sma_kernel<true, false>), grid, dim3(block), lds, st, syms, close, g, out);
+        hipLaunchKernelGGL((sma_kernel<true, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else
-        hipLaunchKernelGGL((sma_kernel<false, false>), grid, dim3(block), lds, st, syms, close, g, out);
+        hipLaunchKernelGGL((sma_kernel<false, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     return hipGetLastError();
 }
 

@@ -248,3 +248,23 @@ def test_config34_grids_long_series(config):
             where = f"config {config} sym {s} {grid.param(p)}"
             compare_summary(got[s, p], orc[p], where)
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.parametrize("nf,ns", [(32, 32), (20, 30), (44, 25), (7, 3)])
+def test_sma_block_shapes(nf, ns):
+    """Every SMA launch shape: 16 waves with the scan folded into a parameter wave (P = 1024,
+    the config-5 grid), a 10-wave block plus helper (600), two equal y-blocks (1100) and a
+    partial single wave (21); long windows (config 5's slow axis reaches 6,400 bars)."""
+    fast = np.arange(1, nf + 1) * 5
+    slow = np.arange(1, ns + 1) * 200
+    grid = D.Grid.sma(fast, slow, annualization=98280)
+    S, bars = 3, 15000
+    with D.Engine(grid) as e:
+        e.load_synthetic(0x5EED, 40, S, bars, D.BT_MINUTE)
+        e.run()
+        got = e.summaries()
+    closes = np.stack([F.gen(0x5EED, 40 + s, bars, 1)[3] for s in range(S)])
+    orc = F.sma_grid_mt(closes, fast, slow, 98280, 8)
+    for s in range(S):
+        for p in range(grid.n_params):
+            compare_summary(got[s, p], orc[s, p], f"shape {nf}x{ns} sym {s} param {p}")
