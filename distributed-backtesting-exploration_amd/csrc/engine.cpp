@@ -160,6 +160,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
         case BT_BOLL: {
             if (!(err = copy_axis(0, c.bwin, c.n_bwin, "bwin", 1, 1 << 16)).empty()) return err;
             if (!(err = copy_axis(1, c.k_num, c.n_k, "k_num", 0, 1 << 20)).empty()) return err;
+            if (c.n_k > 8) return "Bollinger grid: at most 8 k values";
             if (!(err = copy_axis(2, c.sl_bps, c.n_sl, "sl_bps", 0, 9999)).empty()) return err;
             if (!(err = copy_axis(3, c.tp_bps, c.n_tp, "tp_bps", 0, 9999)).empty()) return err;
             if (c.k_den < 1 || c.k_den > (1 << 20)) return "k_den out of range";
@@ -169,6 +170,10 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             e->grid.nd = c.n_tp;
             e->grid.k_den = c.k_den;
             e->grid.wmax = *std::max_element(e->ax[0].begin(), e->ax[0].end());
+            // z tests D^2 kd^2 vs kn^2 Q with D^2, Q < w^2 2^62: exact in int128 while
+            // w * max(k_num, k_den) < 2^32 (spec §4, oracle/oracle.c orc_boll)
+            const int64_t kmax = std::max<int64_t>(c.k_den, *std::max_element(e->ax[1].begin(), e->ax[1].end()));
+            if ((int64_t)e->grid.wmax * kmax >= (1LL << 32)) return "Bollinger grid outside the exact int128 range (window * k >= 2^32)";
             e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
             if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;

@@ -23,6 +23,7 @@
 //   parameter waves, tile k: each lane ANDs its words and walks only its position changes
 //            (ctz), O(1) accounting per change (tile_common.h).
 #include <algorithm>
+#include <cstdlib>
 
 #include "tile_common.h"
 
@@ -33,7 +34,7 @@ namespace {
 constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflict-free columns
 
 struct TileLds {
-    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, total;
+    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, ctr, total;
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks)
@@ -47,15 +48,16 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
     L.ql = take((size_t)kTileStages * 2 * kTile * 8);
     L.dst = take((size_t)kTileStages * kDstLevels * kTile * sizeof(Agg));
     if (kind == 1) {
-        L.stl = take((size_t)kTileStages * kDstLevels * kTile * 4);
-        L.sth = take((size_t)kTileStages * kDstLevels * kTile * 4);
+        L.stl = take((size_t)kTileStages * (2 * kTile + 16) * 4);  // lows, highs, block extrema
+        L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
         L.words = take((size_t)2 * (2 * na * nb + 2 * na) * 8);
         L.win = take((size_t)na * 4);
     } else {
-        L.ebuf = take((size_t)na * kEStride * 8);
+        L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
         L.win = take((size_t)nb * 4);
     }
+    L.ctr = take(4);
     L.total = o;
     return L;
 }
@@ -64,39 +66,32 @@ __device__ __forceinline__ int32_t ldc(const int32_t* __restrict__ row, int B, i
     return t < B ? row[t] : pad;
 }
 
-// First in-tile bar >= a whose low is <= X (64 if none): binary lifting over
-// ST[k][i] = min(low[i .. i + 2^k)).
-__device__ __forceinline__ int first_le(const int32_t* ST, int a, int64_t X) {
-    int pos = a;
-#pragma unroll
-    for (int k = kDstLevels - 1; k >= 0; --k) {
-        const int len = 1 << k;
-        const int32_t v = ST[k * kTile + min(pos, kTile - 1)];
-        pos += (pos + len <= kTile && (int64_t)v > X) ? len : 0;
-    }
-    // the skips sum to at most 63: from bar 0 a tile without a hit stops on bar 63
-    return (pos < kTile && (int64_t)ST[pos] > X) ? kTile : pos;
+// Window task counter: round r owns counter values [r * (n + nwaves), (r + 1) * (n + nwaves)):
+// n successful grabs plus exactly one failing grab per wave (the barrier separates rounds).
+__device__ __forceinline__ uint32_t grab_task(uint32_t* ctr, int lane) {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(ctr, 1u);
+    return __builtin_amdgcn_readlane(v, 0);
 }
 
-// First in-tile bar >= a whose high is >= X: ST[k][i] = max(high[i .. i + 2^k)).
-__device__ __forceinline__ int first_ge(const int32_t* ST, int a, int64_t X) {
-    int pos = a;
-#pragma unroll
-    for (int k = kDstLevels - 1; k >= 0; --k) {
-        const int len = 1 << k;
-        const int32_t v = ST[k * kTile + min(pos, kTile - 1)];
-        pos += (pos + len <= kTile && (int64_t)v < X) ? len : 0;
-    }
-    return (pos < kTile && (int64_t)ST[pos] < X) ? kTile : pos;
-}
+// Bits [cur, 63] of a tile word (none for cur >= 64).
+__device__ __forceinline__ uint64_t bits_from(int cur) { return cur < kTile ? (~0ULL << cur) : 0ULL; }
 
 }  // namespace
 
 // ----------------------------------------------------------------------------- EMA + OLS
-template <bool PARITY>
+// Workgroup = parameter waves + helper A + helper B, one barrier per tile:
+//   helper A, tile k+2: closes -> returns, drawdown sparse table, prefix rings;
+//   helper B, tile k+2: the EMA chains (one sequential fp64 chain per span, lane = span);
+//   every wave, tile k+1, after its own work: condition words, one task per span (4 ballots
+//           over the EMA values) or per OLS window (exact numerator sign), grabbed from an LDS
+//           counter;
+//   parameter waves, tile k: one trade per loop iteration (entry at the first entry bar, exit
+//           at the first exit bar), O(1) accounting per trade.
+template <bool PARITY, bool STAMPS>
 __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
-                                                        Grid g, Out out) {
+                                                        Grid g, Out out, int nextra) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nsp = g.na, nol = g.nb, R = g.ring, RM = g.ring - 1;
     const TileLds LL = tile_lds_layout(0, R, nsp, nol);
@@ -105,12 +100,14 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
-    double* ebuf = reinterpret_cast<double*>(smem + LL.ebuf);
+    double* ebuf = reinterpret_cast<double*>(smem + LL.ebuf);  // [2][nsp][kEStride]
     uint64_t* words = reinterpret_cast<uint64_t*>(smem + LL.words);
     int32_t* win = reinterpret_cast<int32_t*>(smem + LL.win);
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int npw = (int)(blockDim.x >> 6) - 2;
+    // waves: [0, npw) parameters, npw helper A, npw + 1 helper B, then `nextra` task-only waves
+    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 2 - nextra;
     const bool helperA = wave == npw, helperB = wave == npw + 1;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
@@ -120,10 +117,14 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int i_n = pj / nol, i_w = pj % nol;
     const int warm = max(g.a[i_n], g.b[i_w]) - 1;
     const int32_t* crow = close + sd.off;
-    const int nword = 4 * nsp + 2 * nol;
+    const int nword = 4 * nsp + 2 * nol, ntask = nsp + nol;
+    const int estage = nsp * kEStride;
 
     for (int o = tid; o < nol; o += blockDim.x) win[o] = g.b[o];
-    if (tid == 0) r1[0] = r2[0] = 0;
+    if (tid == 0) {
+        r1[0] = r2[0] = 0;
+        *ctr = 0;
+    }
     double alpha = 0.0, ema = 0.0;
     if (helperB && lane < nsp) alpha = 2.0 / ((double)g.a[lane] + 1.0);
     const double lo_mult = (double)(10000 - g.band_bps), hi_mult = (double)(10000 + g.band_bps);
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     uint64_t cy2 = 0;
     int32_t cpre = 0;
 
-    auto scanA = [&](int T, int32_t c) {
+    auto scan = [&](int T, int32_t c) {
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
@@ -143,72 +144,83 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         cy2 += (uint64_t)lane63_i64(inc2);
     };
 
-    auto flagsB = [&](int T) {
-        const int s = T % kTileStages, t1 = T * kTile, t = t1 + lane;
-        const int32_t cl = cts[s * kTile + lane];
-        uint64_t* W = words + (T & 1) * nword;
-        // EMA chains, lane = span: e_t = e_{t-1} + alpha (c_t - e_{t-1}), three roundings
+    // EMA chains of tile T, lane = span, from the tile's closes cl (lane = bar) that helper B
+    // loads itself (no dependency on helper A's scan of the same tile):
+    // e_t = e_{t-1} + alpha (c_t - e_{t-1}), three roundings, e_0 = c_0
+    auto chain = [&](int T, int32_t cl) {
+        const int t1 = T * kTile;
+        double* E = ebuf + (T & 1) * estage + lane * kEStride;
         if (lane < nsp) {
             if (t1 > 0 && t1 + kTile <= B) {
 #pragma unroll
                 for (int b = 0; b < kTile; ++b) {
                     const double cd = (double)__builtin_amdgcn_readlane(cl, b);
                     ema = ema + alpha * (cd - ema);
-                    ebuf[lane * kEStride + b] = ema;
+                    E[b] = ema;
                 }
             } else {
 #pragma unroll 1
                 for (int b = 0; b < kTile; ++b) {
                     const double cd = (double)__builtin_amdgcn_readlane(cl, b);
                     if (t1 + b < B) ema = (t1 + b == 0) ? cd : ema + alpha * (cd - ema);
-                    ebuf[lane * kEStride + b] = ema;
+                    E[b] = ema;
                 }
-            }
-        }
-        // lane = bar from here on
-        const double cd = (double)cl;
-        const double lhs = cd * 10000.0;
-#pragma unroll 1
-        for (int sp = 0; sp < nsp; ++sp) {
-            const double e = ebuf[sp * kEStride + lane];
-            const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
-            const uint64_t wx = __ballot(cd >= e), wy = __ballot(cd <= e);
-            if (lane == 0) {
-                W[4 * sp + 0] = wa;
-                W[4 * sp + 1] = wb;
-                W[4 * sp + 2] = wx;
-                W[4 * sp + 3] = wy;
-            }
-        }
-        // OLS centred numerator N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
-        const uint64_t P1t = r1[(t + 1) & RM], P2t = r2[(t + 1) & RM];
-#pragma unroll 1
-        for (int o = 0; o < nol; ++o) {
-            const int Wn = win[o];
-            const int jj = t + 1 - Wn;
-            const bool valid = jj >= 0 && t < B;
-            const uint64_t S = P1t - r1[jj & RM];
-            const uint64_t Tq = (P2t - r2[jj & RM]) - (uint64_t)(int64_t)jj * S;
-            const int64_t N = (int64_t)(2 * Tq - (uint64_t)(Wn - 1) * S);
-            const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
-            if (lane == 0) {
-                W[4 * nsp + 2 * o] = wp;
-                W[4 * nsp + 2 * o + 1] = wn;
             }
         }
     };
 
-    // prologue: scan tiles 0, 1; flag tile 0
-    if (helperA) {
+    // condition words of tile T, tasks grabbed dynamically (round T), lane = bar
+    auto flags = [&](int T) {
+        const int s = T % kTileStages, t = T * kTile + lane;
+        const int32_t cl = cts[s * kTile + lane];
+        const double cd = (double)cl, lhs = cd * 10000.0;
+        uint64_t* Wd = words + (T & 1) * nword;
+        const double* E = ebuf + (T & 1) * estage;
+        const uint64_t P1t = r1[(t + 1) & RM], P2t = r2[(t + 1) & RM];
+        const uint32_t base = (uint32_t)T * (uint32_t)(ntask + nwaves);
+        uint32_t o = grab_task(ctr, lane) - base;
+#pragma unroll 1
+        while (o < (uint32_t)ntask) {
+            const uint32_t nxt = grab_task(ctr, lane) - base;
+            if ((int)o < nsp) {  // span: entry / exit conditions against the EMA
+                const double e = E[o * kEStride + lane];
+                const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
+                const uint64_t wx = __ballot(cd >= e), wy = __ballot(cd <= e);
+                if (lane == 0) {
+                    Wd[4 * o + 0] = wa;
+                    Wd[4 * o + 1] = wb;
+                    Wd[4 * o + 2] = wx;
+                    Wd[4 * o + 3] = wy;
+                }
+            } else {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
+                const int ow = (int)o - nsp;
+                const int Wn = win[ow];
+                const int jj = t + 1 - Wn;
+                const bool valid = jj >= 0 && t < B;
+                const uint64_t S = P1t - r1[jj & RM];
+                const uint64_t Tq = (P2t - r2[jj & RM]) - (uint64_t)(int64_t)jj * S;
+                const int64_t N = (int64_t)(2 * Tq - (uint64_t)(Wn - 1) * S);
+                const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
+                if (lane == 0) {
+                    Wd[4 * nsp + 2 * ow] = wp;
+                    Wd[4 * nsp + 2 * ow + 1] = wn;
+                }
+            }
+            o = nxt;
+        }
+    };
+
+    // prologue: scan + chain tiles 0, 1; words of tile 0
+    if (helperA || helperB) {
         const int32_t c0 = ldc(crow, B, lane, 0), c1 = ldc(crow, B, kTile + lane, 0);
         cpre = ldc(crow, B, 2 * kTile + lane, 0);
-        scanA(0, c0);
-        __syncthreads();
-        if (ntiles > 1) scanA(1, c1);
-    } else {
-        __syncthreads();
-        if (helperB) flagsB(0);
+        if (helperA) scan(0, c0); else chain(0, c0);
+        if (ntiles > 1) {
+            if (helperA) scan(1, c1); else chain(1, c1);
+        }
     }
+    __syncthreads();
+    flags(0);
     __syncthreads();
 
     TradeAcct a;
@@ -217,13 +229,15 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
 
+    StampAcc sa;
+    if (STAMPS) sa.begin();
     for (int k = 0; k < ntiles; ++k) {
         const int t0 = k * kTile;
-        if (helperA && k + 2 < ntiles) {
-            scanA(k + 2, cpre);
+        if ((helperA || helperB) && k + 2 < ntiles) {
+            if (helperA) scan(k + 2, cpre); else chain(k + 2, cpre);
             cpre = ldc(crow, B, t0 + 3 * kTile + lane, 0);
         }
-        if (helperB && k + 1 < ntiles) flagsB(k + 1);
+        if (STAMPS) sa.mark(0);
         if (active) {
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
@@ -235,46 +249,123 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             const uint64_t Bw = W[4 * i_n + 1] & W[4 * nsp + 2 * i_w + 1] & vm & ~Aw;
             const uint64_t Xw = W[4 * i_n + 2] & vm, Yw = W[4 * i_n + 3] & vm;
             const int bl = B - 1 - t0;
-            const uint64_t fb = (bl >= 0 && bl < kTile) ? (1ULL << bl) : 0ULL;
+            const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;  // forced exit (bl >= 0)
             int cur = 0;
-            while (cur < kTile) {  // one position change per iteration, in bar order
-                const uint64_t el = ~0ULL << cur;
-                const uint64_t m = (a.pos == 0 ? (Aw | Bw) : ((a.pos > 0 ? Xw : Yw) | fb)) & el;
-                if (m == 0) break;
-                const int b = __builtin_ctzll(m);
-                const int t = t0 + b;
-                const int32_t cx = cT[b];
-                const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
+#pragma unroll 1
+            while (true) {  // one trade (entry and/or exit) per iteration, in bar order
+                if (STAMPS) sa.count(3);
                 if (a.pos == 0) {
+                    const uint64_t m = (Aw | Bw) & bits_from(cur);
+                    if (m == 0) break;
+                    const int b = __builtin_ctzll(m);
                     const int np = ((Aw >> b) & 1) ? 1 : -1;
+                    const int32_t cx = cT[b];
+                    const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
                     a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
                     a.ps2 -= q2x;
-                    acct_open(a, t, b, cx);
+                    acct_open(a, t0 + b, b, cx);
                     a.pos = np;
-                } else {
-                    const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, b));
-                    acct_close<PARITY>(a, t, cx, st, tr, cap);
-                    a.ps1 += a.pos > 0 ? qx : (uint64_t)0 - qx;
-                    a.ps2 += q2x;
-                    a.pos = 0;
+                    cur = b + 1;
                 }
-                cur = b + 1;
+                const uint64_t m = ((a.pos > 0 ? Xw : Yw) | fb) & bits_from(cur);
+                if (m == 0) break;
+                const int x = __builtin_ctzll(m);
+                const int32_t cx = cT[x];
+                const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, x));
+                const bool lg = a.pos > 0;
+                acct_close<PARITY>(a, t0 + x, cx, st, tr, cap);
+                a.ps1 += lg ? qx : (uint64_t)0 - qx;
+                a.ps2 += q2x;
+                a.pos = 0;
+                cur = x + 1;
             }
+            if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
         }
+        if (k + 1 < ntiles) flags(k + 1);
+        if (STAMPS) sa.mark(2);
         __syncthreads();
+        if (STAMPS) sa.barrier();
     }
+    if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helperA ? 1 : (helperB ? 2 : 3)), lane);
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
 // ----------------------------------------------------------------------------- Bollinger
-template <bool PARITY>
+// Workgroup = parameter waves + one helper wave, one barrier per tile:
+//   helper, tile k+2: closes/highs/lows -> returns, drawdown sparse table, prefix rings, the raw
+//           lows/highs and their 8-bar block minima/maxima (SL/TP first-passage search);
+//   every wave, tile k+1, after its own work: condition words, one task per window grabbed
+//           from an LDS counter (z tests in fp64 with an exact int128 fallback);
+//   parameter waves, tile k: one trade per loop iteration (entry at the first z signal, exit at
+//           the first of SL/TP / signal / forced), O(1) accounting per trade.
+constexpr int kLH = 2 * kTile + 16;  // per stage: lows[64], highs[64], block min[8], block max[8]
+constexpr int kMaxK = 8;             // z thresholds per window (engine-validated)
+
+// 8-bit mask of v_j > X over a (4+4)-int32 group, bit j = element j: the sign bit of X - v_j
+// (no overflow: prices, padding and levels all lie in [0, 2^31)) shifted in by v_alignbit,
+// two VALU per element.
+__device__ __forceinline__ uint32_t gt8(const int4& a, const int4& b, int32_t X) {
+    uint32_t m = 0;
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - b.w), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - b.z), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - b.y), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - b.x), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - a.w), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - a.z), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - a.y), 31);
+    m = __builtin_amdgcn_alignbit(m, (uint32_t)(X - a.x), 31);
+    return m;
+}
+
+__device__ __forceinline__ int4 ld4(const int32_t* p) { return *reinterpret_cast<const int4*>(p); }
+
+// Keep loaded values live here: the loads above are issued together and not sunk into the
+// divergent branches that consume them.
+__device__ __forceinline__ void pin4(const int4& v) {
+    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+}
+
+// SL/TP first passage from in-tile bar cur (< 64) of an open trade: xlo = first bar whose low
+// is <= XL, xhi = first bar whose high is > XH1 (64 if none). LO/HI: the tile's 64 lows /
+// highs, BX: 8 block minima of the lows then 8 block maxima of the highs. Two dependent LDS
+// round trips for both searches together: the 8-bar block of `cur` and the block extrema,
+// then the first later block that qualifies.
+__device__ __forceinline__ void sltp_search(const int32_t* LO, const int32_t* HI, const int32_t* BX,
+                                            int cur, int32_t XL, int32_t XH1, int& xlo, int& xhi) {
+    const int cb = cur >> 3;
+    const int4 l0 = ld4(LO + 8 * cb), l1 = ld4(LO + 8 * cb + 4);
+    const int4 h0 = ld4(HI + 8 * cb), h1 = ld4(HI + 8 * cb + 4);
+    const int4 n0 = ld4(BX), n1 = ld4(BX + 4), x0 = ld4(BX + 8), x1 = ld4(BX + 12);
+    pin4(l0); pin4(l1); pin4(h0); pin4(h1); pin4(n0); pin4(n1); pin4(x0); pin4(x1);
+    const uint32_t from = (0xFFu << (cur & 7)) & 0xFFu, after = (0xFEu << cb) & 0xFFu;
+    const uint32_t inL = ~gt8(l0, l1, XL) & from, inH = gt8(h0, h1, XH1) & from;
+    const uint32_t laL = ~gt8(n0, n1, XL) & after, laH = gt8(x0, x1, XH1) & after;
+    const int fL = laL ? __builtin_ctz(laL) : cb, fH = laH ? __builtin_ctz(laH) : cb;
+    const int4 a0 = ld4(LO + 8 * fL), a1 = ld4(LO + 8 * fL + 4);
+    const int4 b0 = ld4(HI + 8 * fH), b1 = ld4(HI + 8 * fH + 4);
+    pin4(a0); pin4(a1); pin4(b0); pin4(b1);
+    const uint32_t sL = (~gt8(a0, a1, XL) & 0xFFu) | 0x100u, sH = gt8(b0, b1, XH1) | 0x100u;
+    xlo = inL ? 8 * cb + __builtin_ctz(inL) : (laL ? 8 * fL + __builtin_ctz(sL) : kTile);
+    xhi = inH ? 8 * cb + __builtin_ctz(inH) : (laH ? 8 * fH + __builtin_ctz(sH) : kTile);
+}
+
+// floor(ce * f / 10000) for 0 < ce < 2^31, 0 < f < 2^15 (SL/TP levels, spec §4): the product is
+// exact in fp64 (< 2^46); fl(1e-4) and the product add < 2^-19 absolute error and the 2^-16
+// offset keeps the sum inside [n, n + 1) for every remainder 0..9999.
+__device__ __forceinline__ int64_t level_div(int32_t ce, int32_t f) {
+    const double y = ((double)ce * (double)f) * 1e-4;
+    return (int64_t)floor(y + 0x1p-16);
+}
+
+template <bool PARITY, bool STAMPS>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
                                                          const int32_t* __restrict__ high,
                                                          const int32_t* __restrict__ low,
                                                          const int32_t* __restrict__ close,
-                                                         Grid g, Out out) {
+                                                         Grid g, Out out, int nextra) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring, RM = g.ring - 1;
     const TileLds LL = tile_lds_layout(1, R, nw, nk);
@@ -283,14 +374,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
-    int32_t* stl = reinterpret_cast<int32_t*>(smem + LL.stl);
-    int32_t* sth = reinterpret_cast<int32_t*>(smem + LL.sth);
+    int32_t* lhs_ = reinterpret_cast<int32_t*>(smem + LL.stl);
     uint64_t* words = reinterpret_cast<uint64_t*>(smem + LL.words);
     int32_t* win = reinterpret_cast<int32_t*>(smem + LL.win);
+    double* kn2d = reinterpret_cast<double*>(smem + LL.ebuf);
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int npw = (int)(blockDim.x >> 6) - 2;
-    const bool helperA = wave == npw, helperB = wave == npw + 1;
+    // waves: [0, npw) parameters, npw the helper, then `nextra` task-only waves
+    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra;
+    const bool helper = wave == npw;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
     const int j = blockIdx.y * npw * 64 + tid;
@@ -300,17 +393,20 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int itp = pj % g.nd, isl = (pj / g.nd) % g.nc, ik = (pj / (g.nd * g.nc)) % nk,
               iw = pj / (g.nd * g.nc * nk);
     const int w = g.a[iw];
-    const int64_t sl_bps = g.c[isl], tp_bps = g.d[itp];
+    const int32_t sl_bps = g.c[isl], tp_bps = g.d[itp];
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
     const int nword = 2 * nw * nk + 2 * nw;
-    const i128 kd2 = (i128)((int64_t)g.k_den * g.k_den);
+    const int64_t kd2 = (int64_t)g.k_den * g.k_den;
+    const double kd2d = (double)kd2;
 
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
+    for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
     if (tid == 0) {
         r1[0] = 0;
         r2[0] = 0;
+        *ctr = 0;
     }
     __syncthreads();
 
@@ -318,7 +414,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     unsigned __int128 cy2 = 0;
     int32_t cpre = 0, hpre = 0, lpre = 0;
 
-    auto scanA = [&](int T, int32_t c, int32_t hv, int32_t lv) {
+    auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
@@ -330,107 +426,128 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const unsigned __int128 inc2 = ((unsigned __int128)(uint64_t)shi << 32) + (uint64_t)slo;
         r2[(t + 1) & RM] = cy2 + inc2;
         cy2 += ((unsigned __int128)(uint64_t)lane63_i64(shi) << 32) + (uint64_t)lane63_i64(slo);
-        // low / high sparse tables for SL/TP first-passage search
-        int32_t* SL = stl + s * kDstLevels * kTile;
-        int32_t* SH = sth + s * kDstLevels * kTile;
+        // raw lows / highs and their 8-bar block extrema
+        int32_t* LH = lhs_ + s * kLH;
+        LH[lane] = lv;
+        LH[kTile + lane] = hv;
         int32_t mn = lv, mx = hv;
-        SL[lane] = mn;
-        SH[lane] = mx;
 #pragma unroll
-        for (int m = 1; m < kDstLevels; ++m) {
-            const int d = 1 << (m - 1);
-            mn = min(mn, __shfl_down(mn, d, 64));
-            mx = max(mx, __shfl_down(mx, d, 64));
-            SL[m * kTile + lane] = mn;
-            SH[m * kTile + lane] = mx;
+        for (int d = 1; d < 8; d <<= 1) {
+            mn = min(mn, __shfl_xor(mn, d, 64));
+            mx = max(mx, __shfl_xor(mx, d, 64));
+        }
+        if ((lane & 7) == 0) {
+            LH[2 * kTile + (lane >> 3)] = mn;
+            LH[2 * kTile + 8 + (lane >> 3)] = mx;
         }
     };
 
-    auto flagsB = [&](int T) {
+    // condition words of tile T, windows grabbed dynamically (round T), lane = bar
+    auto flags = [&](int T) {
         const int s = T % kTileStages, t = T * kTile + lane;
         const int64_t c = cts[s * kTile + lane];
-        uint64_t* W = words + (T & 1) * nword;
+        uint64_t* Wd = words + (T & 1) * nword;
         const uint64_t P1t = r1[(t + 1) & RM];
         const unsigned __int128 P2t = r2[(t + 1) & RM];
+        const uint32_t base = (uint32_t)T * (uint32_t)(nw + nwaves);
+        uint32_t o = grab_task(ctr, lane) - base;
 #pragma unroll 1
-        for (int o = 0; o < nw; ++o) {
+        while (o < (uint32_t)nw) {
+            const uint32_t nxt = grab_task(ctr, lane) - base;
             const int Wn = win[o];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
             const int64_t S1 = (int64_t)(P1t - r1[jj & RM]);
-            const i128 S2 = (i128)(P2t - r2[jj & RM]);
+            const unsigned __int128 S2 = P2t - r2[jj & RM];
             const int64_t Dv = (int64_t)Wn * c - S1;
-            const i128 Q = (i128)Wn * S2 - (i128)S1 * (i128)S1;
-            const i128 lhs = (i128)Dv * (i128)Dv * kd2;
-#pragma unroll 1
-            for (int q = 0; q < nk; ++q) {
-                const int64_t kn = g.b[q];
-                const i128 rhs = (i128)(kn * kn) * Q;
-                const bool big = valid && lhs > rhs;
-                const uint64_t zl = __ballot(big && Dv < 0), zh = __ballot(big && Dv > 0);
+            const i128 Q = (i128)Wn * (i128)S2 - (i128)S1 * (i128)S1;  // >= 0 on valid bars
+            // fp64 fast path: |z| > k <=> Dv^2 kd^2 > kn^2 Q, both sides within 2^-50 relative
+            const double Dd = (double)Dv;
+            const double lh = (Dd * Dd) * kd2d;
+            // Q < 2^87: (Q >> 32) < 2^55 rounds once, the low word adds one more rounding
+            const double Qd = (double)(int64_t)(Q >> 32) * 0x1p32 + (double)(uint32_t)Q;
+#pragma unroll
+            for (int q = 0; q < kMaxK; ++q) {
+                if (q >= nk) break;
+                const double rh = kn2d[q] * Qd;
+                // lh and rh are within 2^-50 relative of the exact sides: outside a 2^-48 band
+                // the fp64 order is the exact order (both zero lands in the band)
+                bool big = lh > rh * (1.0 + 0x1p-48);
+                const bool amb = valid && !big && !(lh < rh * (1.0 - 0x1p-48));
+                if (__ballot(amb)) {  // rare: settle the whole wave exactly in int128
+                    const int64_t kn = g.b[q];
+                    big = (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * Q;
+                }
+                const uint64_t zl = __ballot(valid && big && Dv < 0);
+                const uint64_t zh = __ballot(valid && big && Dv > 0);
                 if (lane == 0) {
-                    W[2 * (o * nk + q)] = zl;
-                    W[2 * (o * nk + q) + 1] = zh;
+                    Wd[2 * ((int)o * nk + q)] = zl;
+                    Wd[2 * ((int)o * nk + q) + 1] = zh;
                 }
             }
             const uint64_t dp = __ballot(valid && Dv >= 0), dn = __ballot(valid && Dv <= 0);
             if (lane == 0) {
-                W[2 * nw * nk + 2 * o] = dp;
-                W[2 * nw * nk + 2 * o + 1] = dn;
+                Wd[2 * nw * nk + 2 * o] = dp;
+                Wd[2 * nw * nk + 2 * o + 1] = dn;
             }
+            o = nxt;
         }
     };
 
-    if (helperA) {
+    if (helper) {
         const int32_t c0 = ldc(crow, B, lane, 0), c1 = ldc(crow, B, kTile + lane, 0);
-        const int32_t h0 = ldc(hrow, B, lane, INT32_MIN), h1 = ldc(hrow, B, kTile + lane, INT32_MIN);
+        const int32_t h0 = ldc(hrow, B, lane, 0), h1 = ldc(hrow, B, kTile + lane, 0);
         const int32_t l0 = ldc(lrow, B, lane, INT32_MAX), l1 = ldc(lrow, B, kTile + lane, INT32_MAX);
         cpre = ldc(crow, B, 2 * kTile + lane, 0);
-        hpre = ldc(hrow, B, 2 * kTile + lane, INT32_MIN);
+        hpre = ldc(hrow, B, 2 * kTile + lane, 0);
         lpre = ldc(lrow, B, 2 * kTile + lane, INT32_MAX);
-        scanA(0, c0, h0, l0);
+        scan(0, c0, h0, l0);
         __syncthreads();
-        if (ntiles > 1) scanA(1, c1, h1, l1);
+        if (ntiles > 1) scan(1, c1, h1, l1);
     } else {
         __syncthreads();
-        if (helperB) flagsB(0);
     }
+    flags(0);
     __syncthreads();
 
     TradeAcct a;
     acct_init(a);
-    int64_t lv_sl = 0, lv_tp = 0;  // SL / TP levels of the open trade (ticks)
+    // open trade: lows <= XL hit the low-side level, highs > XHm1 the high-side level
+    int32_t XL = 0, XHm1 = 0;
     const size_t gi = (size_t)blockIdx.x * P + pj;
     bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
 
+    StampAcc sa;
+    if (STAMPS) sa.begin();
     for (int k = 0; k < ntiles; ++k) {
         const int t0 = k * kTile;
-        if (helperA && k + 2 < ntiles) {
-            scanA(k + 2, cpre, hpre, lpre);
+        if (helper && k + 2 < ntiles) {
+            scan(k + 2, cpre, hpre, lpre);
             const int tn = t0 + 3 * kTile + lane;
             cpre = ldc(crow, B, tn, 0);
-            hpre = ldc(hrow, B, tn, INT32_MIN);
+            hpre = ldc(hrow, B, tn, 0);
             lpre = ldc(lrow, B, tn, INT32_MAX);
         }
-        if (helperB && k + 1 < ntiles) flagsB(k + 1);
-        if (active) {
+        if (STAMPS) sa.mark(0);
+        if (active && !(g.ablate & 8)) {
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
             const Agg* D = dst + s * kDstLevels * kTile;
-            const int32_t* SL = stl + s * kDstLevels * kTile;
-            const int32_t* SH = sth + s * kDstLevels * kTile;
+            const int32_t* LO = lhs_ + s * kLH;
+            const int32_t* HI = LO + kTile;
             const uint64_t* W = words + (k & 1) * nword;
             const uint64_t vm = bar_range_mask(t0, w - 1, B - 2);
             const uint64_t ZL = W[2 * (iw * nk + ik)] & vm, ZH = W[2 * (iw * nk + ik) + 1] & vm;
             const uint64_t DP = W[2 * nw * nk + 2 * iw] & vm, DN = W[2 * nw * nk + 2 * iw + 1] & vm;
-            const int bl = B - 1 - t0;
+            const int bl = B - 1 - t0;  // forced exit bar (>= 0; in this tile iff < 64)
             int cur = 0;
-            while (cur < kTile) {
-                const uint64_t el = ~0ULL << cur;
-                if (a.pos == 0) {  // entry at the first flagged bar
-                    const uint64_t m = (ZL | ZH) & el;
+#pragma unroll 1
+            while (true) {  // one trade (entry and/or exit) per iteration, in bar order
+                if (STAMPS) sa.count(3);
+                if (a.pos == 0) {
+                    const uint64_t m = (ZL | ZH) & bits_from(cur);
                     if (m == 0) break;
                     const int b = __builtin_ctzll(m);
                     const int np = ((ZL >> b) & 1) ? 1 : -1;
@@ -440,49 +557,65 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     a.ps2 -= q2x;
                     acct_open(a, t0 + b, b, cx);
                     a.pos = np;
-                    const int64_t ce = cx;
-                    lv_sl = np > 0 ? ce * (10000 - sl_bps) / 10000 : ce * (10000 + sl_bps) / 10000;
-                    lv_tp = np > 0 ? ce * (10000 + tp_bps) / 10000 : ce * (10000 - tp_bps) / 10000;
+                    // low-side level: long SL / short TP; high-side: long TP / short SL (< 2^46)
+                    const int64_t xl = level_div(cx, np > 0 ? 10000 - sl_bps : 10000 - tp_bps);
+                    const int64_t xh = level_div(cx, np > 0 ? 10000 + tp_bps : 10000 + sl_bps);
+                    XL = (int32_t)xl;
+                    XHm1 = (int32_t)min(xh - 1, (int64_t)INT32_MAX);
                     cur = b + 1;
-                } else {  // exit: first of SL/TP (intrabar, from entry+1), forced, signal
-                    const bool lg = a.pos > 0;
-                    const uint64_t sig = (lg ? DP : DN) & el;
-                    int x = sig ? __builtin_ctzll(sig) : kTile;
-                    if (bl >= cur && bl < kTile) x = min(x, bl);
-                    const int xsl = lg ? first_le(SL, cur, lv_sl) : first_ge(SH, cur, lv_sl);
-                    const int xtp = lg ? first_ge(SH, cur, lv_tp) : first_le(SL, cur, lv_tp);
-                    const int xs = min(xsl, xtp);
-                    int32_t px;
-                    Agg st;
-                    if (xs < kTile && xs <= x) {  // SL wins a tie with TP; both beat the close
-                        x = xs;
-                        px = (int32_t)(xsl <= xtp ? lv_sl : lv_tp);
-                        const Agg before = x > a.sb ? dst_query_bf(D, a.sb, x - 1) : kAggId;
-                        st = agg_merge(agg_merge(a.agg, before), agg_one(px));
-                    } else if (x < kTile) {
-                        px = cT[x];
-                        st = agg_merge(a.agg, dst_query_bf(D, a.sb, x));
-                    } else {
-                        break;
-                    }
-                    const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                    acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
-                    a.ps1 += lg ? qx : (uint64_t)0 - qx;
-                    a.ps2 += q2x;
-                    a.pos = 0;
-                    cur = x + 1;
                 }
+                if (cur >= kTile) break;
+                // exit: first of SL/TP (intrabar, from entry + 1; SL wins a same-bar tie), the
+                // signal exit and the forced exit at B-1 (SL/TP beat both on the same bar)
+                const bool lg = a.pos > 0;
+                const uint64_t sig = (lg ? DP : DN) & bits_from(cur);
+                int x = sig ? __builtin_ctzll(sig) : kTile;
+                if (bl >= cur && bl < kTile) x = min(x, bl);
+                int xlo, xhi;
+                sltp_search(LO, HI, LO + 2 * kTile, cur, XL, XHm1, xlo, xhi);
+                const int xs = min(xlo, xhi);
+                int32_t px;
+                Agg st;
+                if (xs < kTile && xs <= x) {
+                    x = xs;
+                    px = (xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1;
+                    const Agg before = x > a.sb ? dst_query_bf(D, a.sb, x - 1) : kAggId;
+                    st = agg_merge(agg_merge(a.agg, before), agg_one(px));
+                } else if (x < kTile) {
+                    px = cT[x];
+                    st = agg_merge(a.agg, dst_query_bf(D, a.sb, x));
+                } else {
+                    break;
+                }
+                const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
+                a.ps1 += lg ? qx : (uint64_t)0 - qx;
+                a.ps2 += q2x;
+                a.pos = 0;
+                cur = x + 1;
             }
+            if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
         }
+        if (k + 1 < ntiles && !(g.ablate & 2)) flags(k + 1);
+        if (STAMPS) sa.mark(2);
         __syncthreads();
+        if (STAMPS) sa.barrier();
     }
+    if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helper ? 1 : 3), lane);
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
 // ----------------------------------------------------------------------------- launchers
-static int tile_param_waves(int P) { return std::min((P + 63) / 64, 1024 / 64 - 2); }
+// Extra task-only waves per block (they take condition-word tasks only). The EMA kernel has one
+// parameter wave per symbol on config 3 and is latency-bound at ~1.5 waves per SIMD: two extra
+// waves take 4.96 -> 3.68 ms. The Bollinger kernel already runs 5 waves x 2 blocks per CU and
+// its 122 VGPRs cap a CU at 16 waves: extra waves only cost it (12.4 -> 12.9 ms with 2).
+static int tile_extra_waves(int used, int x) {
+    if (const char* v = getenv("BT_XW")) x = atoi(v);  // tuning aid
+    return std::max(0, std::min(x, 16 - used));
+}
 
 size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
 size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g.nb).total; }
@@ -490,14 +623,17 @@ size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = tile_param_waves(g.n_params);
+    const int pw = std::min((g.n_params + 63) / 64, 1024 / 64 - 2);
+    const int xw = tile_extra_waves(pw + 2, 2);
     const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
-    const dim3 block(64 * (pw + 2));
+    const dim3 block(64 * (pw + 2 + xw));
     const size_t lds = ema_lds_bytes(g);
-    if (parity)
-        hipLaunchKernelGGL(ema_tile_kernel<true>, grid, block, lds, st, syms, close, g, out);
+    if (g.ablate & 64)
+        hipLaunchKernelGGL((ema_tile_kernel<false, true>), grid, block, lds, st, syms, close, g, out, xw);
+    else if (parity)
+        hipLaunchKernelGGL((ema_tile_kernel<true, false>), grid, block, lds, st, syms, close, g, out, xw);
     else
-        hipLaunchKernelGGL(ema_tile_kernel<false>, grid, block, lds, st, syms, close, g, out);
+        hipLaunchKernelGGL((ema_tile_kernel<false, false>), grid, block, lds, st, syms, close, g, out, xw);
     return hipGetLastError();
 }
 
@@ -505,14 +641,17 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
                        hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = tile_param_waves(g.n_params);
+    const int pw = std::min((g.n_params + 63) / 64, 1024 / 64 - 1);
+    const int xw = tile_extra_waves(pw + 1, 0);
     const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
-    const dim3 block(64 * (pw + 2));
+    const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
-    if (parity)
-        hipLaunchKernelGGL(boll_tile_kernel<true>, grid, block, lds, st, syms, high, low, close, g, out);
+    if (g.ablate & 64)
+        hipLaunchKernelGGL((boll_tile_kernel<false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw);
+    else if (parity)
+        hipLaunchKernelGGL((boll_tile_kernel<true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw);
     else
-        hipLaunchKernelGGL(boll_tile_kernel<false>, grid, block, lds, st, syms, high, low, close, g, out);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw);
     return hipGetLastError();
 }
 

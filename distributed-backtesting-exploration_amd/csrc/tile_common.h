@@ -148,6 +148,39 @@ __device__ __forceinline__ void acct_write(const TradeAcct& a, int bars, double 
     if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
 }
 
+// Diagnostic s_memtime stamps (Grid::ablate & 64 builds only): per role (0 = parameter waves,
+// 1 = helper A, 2 = helper B) the cycles spent working and waiting at the tile barrier.
+// dbg[8 * role + {0, 1, 2..5, 7}] = work, barrier, marked segments / counts, waves.
+struct StampAcc {
+    uint64_t prev = 0, w = 0, b = 0, x[4] = {0, 0, 0, 0};
+    __device__ __forceinline__ void begin() { prev = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void mark(int i) {  // work segment i (counted into w as well)
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        x[i] += now - prev;
+        w += now - prev;
+        prev = now;
+    }
+    __device__ __forceinline__ void count(int i) { x[i] += 1; }
+    __device__ __forceinline__ void work() {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        w += now - prev;
+        prev = now;
+    }
+    __device__ __forceinline__ void barrier() {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        b += now - prev;
+        prev = now;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* dbg, int role, int lane) {
+        if (lane == 0 && dbg != nullptr) {
+            atomicAdd(&dbg[8 * role + 0], (unsigned long long)w);
+            atomicAdd(&dbg[8 * role + 1], (unsigned long long)b);
+            for (int i = 0; i < 4; ++i) atomicAdd(&dbg[8 * role + 2 + i], (unsigned long long)x[i]);
+            atomicAdd(&dbg[8 * role + 7], 1ULL);
+        }
+    }
+};
+
 // Decision-bar mask of a tile: bits for bars t0+b with lo <= t0+b <= hi.
 __device__ __forceinline__ uint64_t bar_range_mask(int t0, int lo, int hi) {
     const int a = lo - t0, b = hi - t0;

@@ -1,0 +1,26 @@
+"""Profiling aid: per-role cycle shares of the tile kernels (diagnostic s_memtime build,
+BT_ABLATE=64) on the config-3 / config-4 per-GPU shard. Shares only — stamps perturb the
+schedule (cdna_hip_programming.md §7).   python scripts/stamps_tile.py 3|4"""
+import ctypes as C, os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["BT_ABLATE"] = os.environ.get("BT_ABLATE", "64")
+import dbx_amd as D
+from dbx_amd import engine as E
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 500
+L = E.lib(); L.bt_read_debug.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+grid = D.config3_grid() if cfg == 3 else D.config4_grid()
+bars = 98280
+ntiles = (bars + 63) // 64
+e = D.Engine(grid, timing=True)
+e.load_synthetic(0x5EED, 0, S, bars, D.BT_MINUTE)
+e.run(); e.sync()
+buf = (C.c_uint64 * 32)()
+L.bt_read_debug(e._h, buf, 32)
+for role, who in enumerate(("param waves", "helper A (scan)", "helper B (chain)", "task waves")):
+    n = max(buf[8 * role + 7], 1)
+    w, b = buf[8 * role] / n / ntiles, buf[8 * role + 1] / n / ntiles
+    x = [buf[8 * role + 2 + i] / n / ntiles for i in range(4)]
+    print(f"config {cfg} {who:18s} waves {buf[8*role+7]:6d}  work {w:7.0f}  barrier {b:7.0f} cyc/tile"
+          f"  [setup {x[0]:.0f} walk {x[1]:.0f} tile-end {x[2]:.0f} iters {x[3]:.2f}]")
+ms, nl, _ = e.kernel_timing(); print("kernel ms (stamped build)", ms / max(nl, 1))
