@@ -1,4 +1,4 @@
-// csv.h — host-side ingest of Job.File bytes (spec §2).
+// csv.h — host-side ingest of Job.File bytes (spec §2): CSV text or binary columns.
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
@@ -15,5 +15,16 @@ struct Bars {
 };
 
 bool parse_csv(const uint8_t* buf, size_t len, Bars& out, std::string& err);
+
+// Binary columnar payload (payload.cpp): detection, decode, encode, host generator.
+bool is_binary_payload(const uint8_t* buf, size_t len);
+size_t binary_payload_size(int32_t n, bool volume);
+bool parse_binary(const uint8_t* buf, size_t len, Bars& out, std::string& err);
+// Job.File in either format (CSV or binary columns), dispatched on the magic.
+bool parse_job(const uint8_t* buf, size_t len, Bars& out, std::string& err);
+size_t encode_binary(const int32_t* o, const int32_t* h, const int32_t* l, const int32_t* c,
+                     const int64_t* v, int32_t n, uint8_t* out);
+void gen_host(uint64_t seed, int64_t sym, int32_t bars, int32_t freq, int32_t* o, int32_t* h,
+              int32_t* l, int32_t* c, int64_t* v);
 
 }  // namespace bt

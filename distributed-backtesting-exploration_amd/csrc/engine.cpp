@@ -682,7 +682,7 @@ int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* 
         auto work = [&]() {
             for (size_t i; (i = next.fetch_add(1)) < n;) {
                 try {
-                    ok[i] = parse_csv(jobs[i].file, jobs[i].len, bars[i], errs[i]) ? 1 : 0;
+                    ok[i] = parse_job(jobs[i].file, jobs[i].len, bars[i], errs[i]) ? 1 : 0;
                 } catch (...) {
                     errs[i] = "parse failure";
                     ok[i] = 0;
@@ -777,10 +777,41 @@ double bt_i128_to_double(uint64_t lo, int64_t hi) { return i128_to_double(lo, hi
 
 int32_t bt_parse_csv(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
                      int32_t* c, char* err, size_t errlen) {
+    return bt_parse_job(buf, len, cap, h, l, c, err, errlen);
+}
+
+int64_t bt_encode_columns(const int32_t* o, const int32_t* h, const int32_t* l, const int32_t* c,
+                          const int64_t* v, int32_t n, uint8_t* out, size_t cap) {
+    ABI_GUARD(-1, {
+        if (n < 1 || n > kMaxBars || !o || !h || !l || !c) throw HipFail{"bad arguments"};
+        const size_t need = binary_payload_size(n, v != nullptr);
+        if (!out) return (int64_t)need;
+        if (cap < need) throw HipFail{"output buffer too small"};
+        return (int64_t)encode_binary(o, h, l, c, v, n, out);
+    })
+}
+
+int64_t bt_gen_payload(uint64_t seed, int64_t sym, int32_t bars, int32_t freq, uint8_t* out,
+                       size_t cap) {
+    ABI_GUARD(-1, {
+        if (bars < 1 || bars > kMaxBars || (freq != BT_DAILY && freq != BT_MINUTE))
+            throw HipFail{"bad arguments"};
+        const size_t need = binary_payload_size(bars, true);
+        if (!out) return (int64_t)need;
+        if (cap < need) throw HipFail{"output buffer too small"};
+        std::vector<int32_t> o((size_t)bars), h((size_t)bars), l((size_t)bars), c((size_t)bars);
+        std::vector<int64_t> v((size_t)bars);
+        gen_host(seed, sym, bars, freq, o.data(), h.data(), l.data(), c.data(), v.data());
+        return (int64_t)encode_binary(o.data(), h.data(), l.data(), c.data(), v.data(), bars, out);
+    })
+}
+
+int32_t bt_parse_job(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
+                     int32_t* c, char* err, size_t errlen) {
     ABI_GUARD(-1, {
         Bars b;
         std::string m;
-        if (!parse_csv(buf, len, b, m)) {
+        if (!parse_job(buf, len, b, m)) {
             if (err && errlen) snprintf(err, errlen, "%s", m.c_str());
             set_err(m);
             return -1;

@@ -14,10 +14,20 @@ Mirrored semantics:
   * replies gzip-compressed                                                main.rs:212
 Known reference quirk kept visible, not copied: peers are keyed by the server's own
 local_addr (main.rs:84,109); here they are keyed by the client's peer string.
+
+Additions (the reference's known gaps, README.md:80-82):
+  * results sink: every CompleteRequest.data is kept and, with `results_path`, appended as one
+    JSON line {"id", "path", "data"} (the reference drops `data`, main.rs:70,76);
+  * re-dispatch on worker loss: jobs handed to a peer that the health thread prunes (silent
+    > 10 s) go back to the queue and are handed out again under new ids; a late completion of
+    an old id is still recorded, and each path's first completion wins;
+  * `gzip=False` serves uncompressed replies (binary columnar payloads, §8(f) row 1, gain little
+    from gzip and its CPU cost would bound a gRPC-fed sweep).
 """
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import threading
 import time
@@ -47,15 +57,22 @@ def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
 
 
 class Dispatcher:
-    def __init__(self, paths: List[str], prune_after_s: float = 10.0, check_every_s: float = 0.1):
+    def __init__(self, paths: List[str], prune_after_s: float = 10.0, check_every_s: float = 0.1,
+                 results_path: Optional[str] = None):
         self.files = list(paths)
+        self.n_paths = len(set(paths))
         self.files_lock = threading.Lock()
         self.peers: Dict[str, dict] = {}
         self.peers_lock = threading.Lock()
         self.jobs_completed: Dict[str, bool] = {}
         self.results: Dict[str, str] = {}      # results sink (the reference ignores data)
         self.job_paths: Dict[str, str] = {}
+        self.inflight: Dict[str, tuple] = {}   # id -> (peer, path) until completed
+        self.done_paths: Dict[str, str] = {}   # path -> id of its first completion
+        self.requeued = 0
         self.done_lock = threading.Lock()
+        self.results_path = results_path
+        self._sink = open(results_path, "a", encoding="utf-8") if results_path else None
         self._stop = threading.Event()
         self.prune_after_s = prune_after_s
         threading.Thread(target=self._health, args=(check_every_s,), daemon=True).start()
@@ -63,21 +80,52 @@ class Dispatcher:
     def _health(self, every):
         while not self._stop.is_set():
             now = time.time()
+            lost = []
             with self.peers_lock:
                 for addr, peer in list(self.peers.items()):
                     if now - peer["last_connection"] > self.prune_after_s:
                         log.info("Removing addr %s", addr)
                         del self.peers[addr]
+                        lost.append(addr)
+            if lost:
+                self._requeue(set(lost))
             time.sleep(every)
+
+    def _requeue(self, peers):
+        with self.done_lock:
+            back = [(jid, path) for jid, (peer, path) in self.inflight.items()
+                    if peer in peers and path not in self.done_paths]
+            for jid, _ in back:
+                del self.inflight[jid]
+        if back:
+            with self.files_lock:
+                self.files.extend(path for _, path in back)
+            self.requeued += len(back)
+            log.info("Re-dispatching %d jobs of lost peers", len(back))
+
+    def all_done(self) -> bool:
+        with self.done_lock:
+            return len(self.done_paths) >= self.n_paths
 
     def close(self):
         self._stop.set()
+        if self._sink:
+            self._sink.close()
+            self._sink = None
 
     # ---- RPC handlers
     def complete_job(self, req, ctx):
         with self.done_lock:
             self.jobs_completed[req.id] = True
             self.results[req.id] = req.data
+            self.inflight.pop(req.id, None)
+            path = self.job_paths.get(req.id)
+            first = path is not None and path not in self.done_paths
+            if first:
+                self.done_paths[path] = req.id
+            if self._sink and first:
+                self._sink.write(json.dumps({"id": req.id, "path": path, "data": req.data}) + "\n")
+                self._sink.flush()
         return P.CompleteReply()
 
     def send_status(self, req, ctx):
@@ -105,13 +153,16 @@ class Dispatcher:
                     data = f.read()
             except OSError:
                 continue
-            self.job_paths[jid] = path
+            with self.done_lock:
+                self.job_paths[jid] = path
+                self.inflight[jid] = (ctx.peer(), path)
             jobs.append(P.Job(id=jid, File=data))
         log.info("Num files to run: %d", len(jobs))
         return P.JobsReply(jobs=jobs)
 
 
-def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20):
+def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20,
+          gzip: bool = True):
     ser = lambda m: m.SerializeToString()  # noqa: E731
     handlers = {
         "CompleteJob": grpc.unary_unary_rpc_method_handler(
@@ -125,7 +176,7 @@ def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 
             response_serializer=ser),
     }
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=8),
-                         compression=grpc.Compression.Gzip,
+                         compression=grpc.Compression.Gzip if gzip else grpc.Compression.NoCompression,
                          options=[("grpc.max_send_message_length", max_send)])
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(P.SERVICE, handlers),))
     port = server.add_insecure_port(addr)
@@ -135,13 +186,26 @@ def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description="backtest job dispatcher")
-    ap.add_argument("paths", nargs="+")
+    ap.add_argument("paths", nargs="+", help="files (CSV or DBXCOL1 payloads) or directories")
     ap.add_argument("--addr", default="[::1]:50051")  # main.rs:195
+    ap.add_argument("--results", default=None, help="append {id, path, data} JSON lines here")
+    ap.add_argument("--no-gzip", action="store_true")
+    ap.add_argument("--max-send-mb", type=int, default=64)
+    ap.add_argument("--exit-when-done", action="store_true")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
-    d = Dispatcher(a.paths)
-    server, _ = serve(d, a.addr)
-    server.wait_for_termination()
+    import os
+    paths = []
+    for p in a.paths:
+        paths += sorted(os.path.join(p, f) for f in os.listdir(p)) if os.path.isdir(p) else [p]
+    d = Dispatcher(paths, results_path=a.results)
+    server, _ = serve(d, a.addr, max_send=a.max_send_mb << 20, gzip=not a.no_gzip)
+    try:
+        while not (a.exit_when_done and d.all_done()):
+            time.sleep(0.1)
+    finally:
+        server.stop(1)
+        d.close()
 
 
 if __name__ == "__main__":

@@ -117,6 +117,11 @@ def lib():
     L.bt_i128_to_double.restype = C.c_double
     L.bt_parse_csv.argtypes = [C.c_char_p, C.c_size_t, C.c_int32, P, P, P, C.c_char_p,
                                C.c_size_t]
+    L.bt_parse_job.argtypes = L.bt_parse_csv.argtypes
+    L.bt_encode_columns.argtypes = [P, P, P, P, P, C.c_int32, P, C.c_size_t]
+    L.bt_encode_columns.restype = C.c_int64
+    L.bt_gen_payload.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, P, C.c_size_t]
+    L.bt_gen_payload.restype = C.c_int64
     _lib = L
     return L
 
@@ -354,10 +359,11 @@ def i128_to_double(lo: int, hi: int) -> float:
 
 
 def parse_csv(data: bytes, cap=1 << 22):
+    """Host ingest of one Job.File (CSV or binary columns) -> (high, low, close) int32 ticks."""
     cap = int(cap)
     h, lo, c = (np.empty(cap, np.int32) for _ in range(3))
     err = C.create_string_buffer(256)
-    n = lib().bt_parse_csv(data, len(data), cap, h.ctypes.data, lo.ctypes.data, c.ctypes.data,
+    n = lib().bt_parse_job(data, len(data), cap, h.ctypes.data, lo.ctypes.data, c.ctypes.data,
                            err, 256)
     if n < 0:
         raise ValueError(err.value.decode())

@@ -165,7 +165,21 @@ int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* o
 /* ---- self-test hooks (host-side helpers the tests call without a GPU) */
 double bt_i128_to_double(uint64_t lo, int64_t hi);
 int32_t bt_parse_csv(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
+                     int32_t* c, char* err, size_t errlen);   /* same as bt_parse_job */
+/* Host ingest of one Job.File (CSV or binary columns) into h/l/c ticks;
+ * returns the bar count, or -1 with the message in err. */
+int32_t bt_parse_job(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
                      int32_t* c, char* err, size_t errlen);
+
+/* ---- binary columnar Job.File payload (payload.cpp): "DBXCOL1\n", u32 n_bars, u32 flags
+ * (bit 0: int64 volume follows), then int32 open/high/low/close columns. Both return the byte
+ * size (the required size when out is NULL) or -1. */
+int64_t bt_encode_columns(const int32_t* o, const int32_t* h, const int32_t* l, const int32_t* c,
+                          const int64_t* v, int32_t n, uint8_t* out, size_t cap);
+/* Spec §1 synthetic OHLCV of one symbol generated on the host as a binary payload (the
+ * dispatcher-side producer for gRPC-fed runs; bit-identical to bt_load_synthetic). */
+int64_t bt_gen_payload(uint64_t seed, int64_t sym, int32_t bars, int32_t freq, uint8_t* out,
+                       size_t cap);
 
 #ifdef __cplusplus
 }

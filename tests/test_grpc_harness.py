@@ -154,3 +154,97 @@ def test_process_incoming_job_flag_and_order():
     WK.process_incoming_job(rep, q, proc)
     assert not WK.PROC_FLAG.is_set()       # process.rs:28
     assert [q.get_nowait() for _ in range(5)] == [(str(i), f"r{i}") for i in range(5)]
+
+
+class _Ctx:
+    """Minimal grpc ServicerContext stand-in for direct handler calls."""
+    def __init__(self, peer):
+        self._peer = peer
+
+    def peer(self):
+        return self._peer
+
+    def abort(self, code, msg):
+        raise RuntimeError(msg)
+
+
+def test_dispatcher_redispatches_jobs_of_lost_worker(tmp_path):
+    """jobs held by a worker that stops checking in (pruned after the
+    silence limit, server/main.rs:183-190) go back to the queue; a second worker completes
+    them. The results sink keeps each path's first completion (row 3)."""
+    paths = [str(tmp_path / f"f{i}.csv") for i in range(6)]
+    for p in paths:
+        open(p, "wb").write(b"2020-01-01,1,1,1,1,1\n")
+    sink = tmp_path / "results.jsonl"
+    d = DSP.Dispatcher(paths, prune_after_s=0.3, check_every_s=0.05, results_path=str(sink))
+    try:
+        a = d.request_jobs(P.JobsRequest(cores=4), _Ctx("ipv4:10.0.0.1:1"))   # tail: f4, f5
+        assert [d.job_paths[j.id] for j in a.jobs] == paths[4:]
+        b = d.request_jobs(P.JobsRequest(cores=4), _Ctx("ipv4:10.0.0.2:2"))   # f0..f3
+        for j in b.jobs:
+            d.complete_job(P.CompleteRequest(id=j.id, data="ok-b"), _Ctx("ipv4:10.0.0.2:2"))
+        assert not d.all_done()
+        t0 = time.time()
+        while d.requeued < 2 and time.time() - t0 < 5:
+            # worker B keeps polling (upserting its last_connection); worker A is silent
+            d.peers["ipv4:10.0.0.2:2"]["last_connection"] = time.time()
+            time.sleep(0.05)
+        assert d.requeued == 2 and "ipv4:10.0.0.1:1" not in d.peers
+        c = d.request_jobs(P.JobsRequest(cores=4), _Ctx("ipv4:10.0.0.2:2"))
+        assert sorted(d.job_paths[j.id] for j in c.jobs) == paths[4:]
+        assert {j.id for j in c.jobs}.isdisjoint({j.id for j in a.jobs})    # fresh ids
+        for j in c.jobs:
+            d.complete_job(P.CompleteRequest(id=j.id, data="ok-c"), _Ctx("ipv4:10.0.0.2:2"))
+        d.complete_job(P.CompleteRequest(id=a.jobs[0].id, data="late-a"), _Ctx("x"))  # late
+        assert d.all_done()
+    finally:
+        d.close()
+    rows = [json.loads(x) for x in sink.read_text().splitlines()]
+    assert sorted(r["path"] for r in rows) == sorted(paths)            # one row per path
+    assert all(r["data"] != "late-a" for r in rows)
+
+
+@pytest.mark.gpu
+def test_binary_payload_minute_jobs_end_to_end_gpu(tmp_path):
+    """§8(f) rows 1-2: 1-minute symbols as DBXCOL1 payloads (2.4 MB each, 4 per JobsReply =
+    9.4 MB > grpc's 4 MiB default: the worker raises its receive limit), served without gzip,
+    EMA+OLS grid (config 3) on the GPU engine, results checked against the C oracle."""
+    import orc_ffi as F
+    from dbx_amd import payload as PL
+    bars, n = 98280, 8
+    paths = []
+    for s in range(n):
+        pth = tmp_path / f"S{s}.dbxcol"
+        pth.write_bytes(PL.gen_payload(0x5EED, s, bars, D.BT_MINUTE))
+        paths.append(str(pth))
+    grid = D.config3_grid()
+    disp = DSP.Dispatcher(paths, results_path=str(tmp_path / "res.jsonl"))
+    server, port = DSP.serve(disp, "127.0.0.1:0", gzip=False)
+    with D.Engine(grid) as eng:
+        w = WK.Worker(f"127.0.0.1:{port}", WK.engine_processor(eng), cores=4, job_tick=0.05,
+                      status_tick=0.2, max_receive=64 << 20)
+        th = threading.Thread(target=w.run, daemon=True)
+        t0 = time.time()
+        th.start()
+        try:
+            while not disp.all_done() and time.time() - t0 < 90:
+                time.sleep(0.05)
+        finally:
+            w.stop.set()
+            th.join(10)
+            server.stop(0)
+            disp.close()
+    assert disp.all_done()
+    print(f"{n} x {bars} minute bars over gRPC in {time.time() - t0:.2f} s")
+    rows = [json.loads(x) for x in (tmp_path / "res.jsonl").read_text().splitlines()]
+    for r in rows:
+        s = paths.index(r["path"])
+        o, h, lo, c = F.gen(0x5EED, s, bars, 1)[:4]
+        lines = r["data"].strip().split("\n")
+        assert len(lines) == grid.n_params
+        for p in (0, 9, 27, 63):
+            kw = grid.param(p)
+            ref, _ = F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], 98280)
+            j = json.loads(lines[p])
+            assert j["n"] == int(ref["n_trades"]) and j["pnl"] == int(ref["pnl"])
+            assert float(j["sharpe"]) == float(ref["sharpe"]) and int(j["h"], 16) == int(ref["hash"])
