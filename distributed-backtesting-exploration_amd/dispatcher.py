@@ -58,7 +58,7 @@ def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
 
 class Dispatcher:
     def __init__(self, paths: List[str], prune_after_s: float = 10.0, check_every_s: float = 0.1,
-                 results_path: Optional[str] = None):
+                 results_path: Optional[str] = None, max_reply_bytes: int = 60 << 20):
         self.files = list(paths)
         self.n_paths = len(set(paths))
         self.files_lock = threading.Lock()
@@ -72,6 +72,9 @@ class Dispatcher:
         self.requeued = 0
         self.done_lock = threading.Lock()
         self.results_path = results_path
+        # a JobsReply larger than the server's send limit fails after its files left the queue
+        # (the reference loses them); replies are capped and the overflow goes back to the queue
+        self.max_reply_bytes = max_reply_bytes
         self._sink = open(results_path, "a", encoding="utf-8") if results_path else None
         self._stop = threading.Event()
         self.prune_after_s = prune_after_s
@@ -146,13 +149,19 @@ class Dispatcher:
             # error status here too. Either way the worker ignores it (handlers.rs:59).
             ctx.abort(grpc.StatusCode.NOT_FOUND, "No more jobs available")
         jobs = []
-        for path in files:
+        size = 0
+        for i, path in enumerate(files):
             jid = str(uuid.uuid4())
             try:
                 with open(path, "rb") as f:
                     data = f.read()
             except OSError:
                 continue
+            if jobs and size + len(data) > self.max_reply_bytes:
+                with self.files_lock:
+                    self.files.extend(files[i:])
+                break
+            size += len(data)
             with self.done_lock:
                 self.job_paths[jid] = path
                 self.inflight[jid] = (ctx.peer(), path)
@@ -163,6 +172,7 @@ class Dispatcher:
 
 def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20,
           gzip: bool = True):
+    dispatcher.max_reply_bytes = min(dispatcher.max_reply_bytes, max_send - (1 << 20))
     ser = lambda m: m.SerializeToString()  # noqa: E731
     handlers = {
         "CompleteJob": grpc.unary_unary_rpc_method_handler(

@@ -59,7 +59,8 @@ def process_incoming_job(jobs_reply, complete_send: "queue.Queue", processor: Pr
 class Worker:
     def __init__(self, target: str, processor: Processor, cores: Optional[int] = None,
                  job_tick: float = 0.250, status_tick: float = 1.0,
-                 max_receive: int = 4 * 1024 * 1024):
+                 max_receive: int = 4 * 1024 * 1024, max_batch_bytes: int = 0,
+                 min_batch_jobs: int = 0, linger_s: float = 0.2):
         self.target = target
         self.processor = processor
         # handlers.rs:35 reports num_cpus/2; a GPU worker reports its batch capacity instead
@@ -68,6 +69,14 @@ class Worker:
         self.reply_q: "queue.Queue" = queue.Queue(maxsize=1024)      # main.rs:32
         self.complete_q: "queue.Queue" = queue.Queue(maxsize=1024)   # main.rs:33
         self.stop = threading.Event()
+        # GPU-aware batching: the compute thread merges the JobsReplies
+        # already queued, up to this many payload bytes, into one engine batch (one launch
+        # fills the GPU only with hundreds of symbols); 0 keeps the reference's one reply per
+        # call (main.rs:38-42).
+        self.max_batch_bytes = max_batch_bytes
+        # ... and waits up to `linger_s` for more replies while the batch holds fewer than
+        # `min_batch_jobs` symbols (a launch runs one workgroup per symbol: hundreds fill it)
+        self.min_batch_jobs, self.linger_s = min_batch_jobs, linger_s
         opts = [("grpc.max_receive_message_length", max_receive)]
         self.channel = grpc.insecure_channel(target, options=opts)
         u = self.channel.unary_unary
@@ -86,6 +95,20 @@ class Worker:
                 reply = self.reply_q.get(timeout=0.05)
             except queue.Empty:
                 continue
+            if self.max_batch_bytes > 0:
+                size = sum(len(j.File) for j in reply.jobs)
+                merged = P.JobsReply(jobs=list(reply.jobs))
+                while size < self.max_batch_bytes:
+                    try:
+                        if len(merged.jobs) < self.min_batch_jobs:
+                            more = self.reply_q.get(timeout=self.linger_s)
+                        else:
+                            more = self.reply_q.get_nowait()
+                    except queue.Empty:
+                        break
+                    merged.jobs.extend(more.jobs)
+                    size += sum(len(j.File) for j in more.jobs)
+                reply = merged
             process_incoming_job(reply, self.complete_q, self.processor)
 
     # handlers.rs:14-32
@@ -144,13 +167,18 @@ def main(argv=None):
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--cores", type=int, default=None, help="jobs per RequestJobs")
     ap.add_argument("--max-receive-mb", type=int, default=4)
+    ap.add_argument("--max-batch-mb", type=int, default=0,
+                    help="merge queued JobsReplies into one GPU batch up to this size")
+    ap.add_argument("--min-batch-jobs", type=int, default=0,
+                    help="linger for more replies while a batch has fewer jobs")
     ap.add_argument("--duration", type=float, default=None)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     grid = {"sma": config2_grid, "ema_ols": config3_grid, "boll": config4_grid}[a.strategy]()
     eng = Engine(grid, device=a.device)
     Worker(a.target, engine_processor(eng), a.cores,
-           max_receive=a.max_receive_mb << 20).run(a.duration)
+           max_receive=a.max_receive_mb << 20, max_batch_bytes=a.max_batch_mb << 20,
+           min_batch_jobs=a.min_batch_jobs).run(a.duration)
 
 
 if __name__ == "__main__":

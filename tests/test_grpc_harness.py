@@ -248,3 +248,22 @@ def test_binary_payload_minute_jobs_end_to_end_gpu(tmp_path):
             j = json.loads(lines[p])
             assert j["n"] == int(ref["n_trades"]) and j["pnl"] == int(ref["pnl"])
             assert float(j["sharpe"]) == float(ref["sharpe"]) and int(j["h"], 16) == int(ref["hash"])
+
+
+def test_dispatcher_caps_reply_bytes(tmp_path):
+    """A reply larger than the send limit would fail after its files left the queue; the
+    dispatcher caps each JobsReply by bytes and requeues the overflow."""
+    paths = [str(tmp_path / f"f{i}") for i in range(10)]
+    for p in paths:
+        open(p, "wb").write(b"x" * 1000)
+    d = DSP.Dispatcher(paths, max_reply_bytes=3500)
+    try:
+        r = d.request_jobs(P.JobsRequest(cores=2), _Ctx("a"))          # tail f2..f9, capped
+        assert [d.job_paths[j.id] for j in r.jobs] == paths[2:5]
+        assert d.files == paths[:2] + paths[5:]
+        got = [d.job_paths[j.id] for j in r.jobs]
+        while d.files:
+            got += [d.job_paths[j.id] for j in d.request_jobs(P.JobsRequest(cores=2), _Ctx("a")).jobs]
+        assert sorted(got) == sorted(paths)
+    finally:
+        d.close()
