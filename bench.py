@@ -88,15 +88,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one process per GPU; ranks outnumbering the visible GPUs (a rehearsal on a 1-GPU box)
+        # share devices, and RCCL needs distinct devices, so the k x 24 B exchange then uses gloo
+        ndev = torch.cuda.device_count()
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        device = local % max(ndev, 1)
+        torch.cuda.set_device(device)
+        if ndev >= local_world:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     grid = D.config2_grid()
     P = grid.n_params
-    eng = D.Engine(grid, device=local, topk=TOPK, timing=True)
+    eng = D.Engine(grid, device=device, topk=TOPK, timing=True)
     eng.load_synthetic(SEED, rank * S_PER_GPU, S_PER_GPU, BARS, D.BT_DAILY)
 
     def step():
@@ -126,7 +135,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kms, launches, kname = eng.kernel_timing()
@@ -154,7 +164,8 @@ def main():
             "data": "synthetic (SplitMix64 integer OHLC walk, docs/oracle_spec.md §1, generated in HBM)",
             "config": {"workload": "BASELINE config 2: SMA fast/slow crossover",
                        "symbols_per_gpu": S_PER_GPU, "bars": BARS, "params": P,
-                       "topk": TOPK, "parallelism": f"dp{world} (symbol shards, RCCL top-k gather)"},
+                       "topk": TOPK, "parallelism": f"dp{world} (symbol shards, "
+                       f"{'RCCL' if dist is None or dist.get_backend() == 'nccl' else 'gloo'} top-k gather)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,
