@@ -43,8 +43,8 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
     L.ring = take((size_t)ring * 8);
     L.keys = take((size_t)2 * nw * kKS * 4);
-    L.invw = take((size_t)nw * 8);
-    L.win = take((size_t)nw * 4);
+    L.invw = take((size_t)(nw + 1) * 8);   // + pad: window pairs are read as one 16-B load
+    L.win = take((size_t)(nw + 1) * 4);
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
@@ -108,17 +108,30 @@ __device__ __forceinline__ void stage_scan(int32_t c, int B, int t0, int lane, i
 
 // Stage 2 for one tile: int32 floor keys for every window. lane = bar, so the window length
 // and its reciprocal are wave-uniform and the top of the ring is read once per tile.
-// Windows are handed out dynamically: every wave of the block (helper included) grabs window
-// indices from an LDS counter after its other work for the tile, so waves with few flips to
-// walk compute more keys. Round r owns counter values [r*(nw+nwaves), (r+1)*(nw+nwaves)):
-// nw successful grabs plus exactly one failing grab per wave (the barrier separates rounds).
+// Windows are handed out dynamically, two per grab: every wave of the block (helper included)
+// grabs window pairs from an LDS counter after its other work for the tile, so waves with few
+// flips to walk compute more keys. Round r owns counter values [r*per, (r+1)*per) with
+// per = 2*ceil(nw/2) + 2*nwaves: the pair grabs plus exactly one failing grab per wave (the
+// barrier separates rounds). The next pair's atomic is in flight while the current pair
+// computes (its result is read only at the end of the iteration).
 // Bars without a full window (or past the series end) get key -1 on fast rows and -2 on slow
 // rows: their difference is never 0, so they never look like ties to the compare stage (they
 // are outside every lane's decision mask anyway).
-__device__ __forceinline__ uint32_t grab(uint32_t* ctr, int lane) {
+__device__ __forceinline__ uint32_t grab_issue(uint32_t* ctr, int lane) {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(ctr, 1u);
-    return __builtin_amdgcn_readlane(v, 0);
+    if (lane == 0) v = atomicAdd(ctr, 2u);
+    return v;
+}
+
+// floor(F / W) for the exact window sum F (< 2^53 as a double): one multiply by an
+// approximate reciprocal, then an exact remainder fix-up.
+__device__ __forceinline__ int32_t floor_key(double F, int W, double iw) {
+    const double fl = floor(F * iw);                       // within 1 of floor(F / W)
+    const double r = F - fl * (double)W;                   // exact
+    int32_t key = (int32_t)fl;
+    key -= (int32_t)(r < 0.0);
+    key += (int32_t)(r >= (double)W);
+    return key;
 }
 
 __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R, const double* ring,
@@ -127,22 +140,28 @@ __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R,
     const int t = t0 + lane;
     const double top = ring[(t + 1) & (R - 1)];
     const bool tin = t < B;
-    const uint32_t base = round * (uint32_t)(nw + nwaves);
-    uint32_t w = grab(ctr, lane) - base;
+    const uint32_t per = 2u * (uint32_t)((nw + 1) >> 1) + 2u * (uint32_t)nwaves;
+    const uint32_t base = round * per;
+    uint32_t w = __builtin_amdgcn_readlane(grab_issue(ctr, lane), 0) - base;
 #pragma unroll 1
     while (w < (uint32_t)nw) {
-        const uint32_t nxt = grab(ctr, lane) - base;  // in flight while this window computes
-        const int W = __builtin_amdgcn_readfirstlane(win[w]);
-        const double iw = invw[w];
-        const double F = top - ring[(t + 1 - W) & (R - 1)];  // exact (< 2^53)
-        const double fl = floor(F * iw);                       // within 1 of floor(F / W)
-        const double r = F - fl * (double)W;                   // exact
-        int32_t key = (int32_t)fl;
-        key -= (int32_t)(r < 0.0);
-        key += (int32_t)(r >= (double)W);
-        const bool valid = tin && t + 1 - W >= 0;
-        K[w * kKS + lane] = valid ? key : ((int)w < nf ? -1 : -2);
-        w = nxt;
+        const uint32_t vn = grab_issue(ctr, lane);  // next pair, read at the end
+        // w is even: win[w..w+1] and invw[w..w+1] are one aligned 8-B / 16-B read each (the
+        // LDS regions are padded, so w + 1 == nw reads a pad entry that is never used)
+        const int2 W2 = *reinterpret_cast<const int2*>(win + w);
+        const double2 I2 = *reinterpret_cast<const double2*>(invw + w);
+        const int W0 = __builtin_amdgcn_readfirstlane(W2.x);
+        const bool two = w + 1 < (uint32_t)nw;
+        const int W1 = two ? __builtin_amdgcn_readfirstlane(W2.y) : W0;
+        const double F0 = top - ring[(t + 1 - W0) & (R - 1)];  // exact (< 2^53)
+        const double F1 = top - ring[(t + 1 - W1) & (R - 1)];
+        const int32_t k0 = floor_key(F0, W0, I2.x);
+        K[w * kKS + lane] = (tin && t + 1 - W0 >= 0) ? k0 : ((int)w < nf ? -1 : -2);
+        if (two) {
+            const int32_t k1 = floor_key(F1, W1, I2.y);
+            K[(w + 1) * kKS + lane] = (tin && t + 1 - W1 >= 0) ? k1 : ((int)w + 1 < nf ? -1 : -2);
+        }
+        w = __builtin_amdgcn_readlane(vn, 0) - base;
     }
 }
 
