@@ -60,6 +60,15 @@ def test_config_validation():
         D.Engine(D.Grid.sma([], [10]))
     with pytest.raises(D.BtError, match="annualization"):
         D.Engine(D.Grid.sma([2], [10], annualization=0))
+    with pytest.raises(D.BtError, match="at most 8 k"):
+        D.Engine(D.Grid.boll([20], list(range(1, 10)), [50], [50]))
+    # per-symbol prefix rings live in LDS: windows beyond a CU's 160 KB are refused up front
+    with pytest.raises(D.BtError, match="LDS"):
+        D.Engine(D.Grid.boll([8000], [2], [50], [50]))
+    with pytest.raises(D.BtError, match="spans"):
+        D.Engine(D.Grid.ema_ols(list(range(2, 70)), [10]))
+    with pytest.raises(D.BtError, match="sl_bps"):
+        D.Engine(D.Grid.boll([20], [2], [10000], [50]))
 
 
 def test_i128_to_double_round_to_nearest_even():
