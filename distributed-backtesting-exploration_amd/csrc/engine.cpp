@@ -153,7 +153,8 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             e->grid.nc = e->grid.nd = 1;
             e->grid.band_bps = c.band_bps;
             e->grid.wmax = *std::max_element(e->ax[1].begin(), e->ax[1].end());
-            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
+            // prefix ring: windows + three tiles in flight, a multiple of the tile (k_tile.hip)
+            e->grid.ring = (e->grid.wmax + 4 * kTile - 1) / kTile * kTile;
             if (ema_lds_bytes(e->grid) > 160 * 1024) return "EMA grid needs more LDS than a CU has (OLS windows too long)";
             break;
         }
@@ -174,7 +175,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             // w * max(k_num, k_den) < 2^32 (spec §4, oracle/oracle.c orc_boll)
             const int64_t kmax = std::max<int64_t>(c.k_den, *std::max_element(e->ax[1].begin(), e->ax[1].end()));
             if ((int64_t)e->grid.wmax * kmax >= (1LL << 32)) return "Bollinger grid outside the exact int128 range (window * k >= 2^32)";
-            e->grid.ring = (int32_t)next_pow2((uint32_t)e->grid.wmax + 3 * kTile);
+            e->grid.ring = (e->grid.wmax + 4 * kTile - 1) / kTile * kTile;
             if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;
         }

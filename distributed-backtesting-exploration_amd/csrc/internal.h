@@ -24,7 +24,8 @@ struct Grid {
     int32_t na, nb, nc, nd;        // axis sizes (SMA: fast, slow; EMA: span, ols; BOLL: w,k,sl,tp)
     int32_t band_bps, k_den;
     int32_t wmax;                  // largest window of the grid (prefix ring sizing)
-    int32_t ring;                  // prefix ring length (power of two >= wmax + 3 kTile)
+    int32_t ring;                  // prefix ring length >= wmax + 3 kTile (SMA: a power of two;
+                                   // tile kernels: a multiple of kTile)
     double sqrt_ann;               // sqrt((double)annualization), computed on the host
     int32_t ablate;                // profiling only (env BT_ABLATE): phases to skip, 0 = none
     const int32_t* a;              // device arrays

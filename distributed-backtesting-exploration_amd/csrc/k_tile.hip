@@ -74,6 +74,18 @@ __device__ __forceinline__ uint32_t grab_task(uint32_t* ctr, int lane) {
     return __builtin_amdgcn_readlane(v, 0);
 }
 
+// Prefix rings: entry x (the sum over bars < x) lives at x mod R, with R a multiple of 64 of at
+// least the longest window + 3 tiles (engine.cpp), so windows up to the spec's 4,096 bars fit
+// in LDS. Position of x = T*64 + lane + 1, and of x - W given that position (0 < W < R).
+__device__ __forceinline__ int ring_pos(int T, int lane, int R) {
+    const int p = (T % (R / kTile)) * kTile + lane + 1;
+    return p == R ? 0 : p;
+}
+__device__ __forceinline__ int ring_back(int p, int W, int R) {
+    const int q = p - W;
+    return q < 0 ? q + R : q;
+}
+
 // Bits [cur, 63] of a tile word (none for cur >= 64).
 __device__ __forceinline__ uint64_t bits_from(int cur) { return cur < kTile ? (~0ULL << cur) : 0ULL; }
 
@@ -93,7 +105,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                                                         const int32_t* __restrict__ close,
                                                         Grid g, Out out, int nextra) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nsp = g.na, nol = g.nb, R = g.ring, RM = g.ring - 1;
+    const int nsp = g.na, nol = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(0, R, nsp, nol);
     uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);  // sum_{i<x} c_i
     uint64_t* r2 = reinterpret_cast<uint64_t*>(smem + LL.r2);  // sum_{i<x} i*c_i (mod 2^64)
@@ -138,9 +150,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
-        r1[(t + 1) & RM] = (uint64_t)pre;
+        const int pt = ring_pos(T, lane, R);
+        r1[pt] = (uint64_t)pre;
         const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end
-        r2[(t + 1) & RM] = cy2 + (uint64_t)inc2;
+        r2[pt] = cy2 + (uint64_t)inc2;
         cy2 += (uint64_t)lane63_i64(inc2);
     };
 
@@ -176,7 +189,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const double cd = (double)cl, lhs = cd * 10000.0;
         uint64_t* Wd = words + (T & 1) * nword;
         const double* E = ebuf + (T & 1) * estage;
-        const uint64_t P1t = r1[(t + 1) & RM], P2t = r2[(t + 1) & RM];
+        const int ptop = ring_pos(T, lane, R);
+        const uint64_t P1t = r1[ptop], P2t = r2[ptop];
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + nwaves);
         uint32_t o = grab_task(ctr, lane) - base;
 #pragma unroll 1
@@ -197,8 +211,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 const int Wn = win[ow];
                 const int jj = t + 1 - Wn;
                 const bool valid = jj >= 0 && t < B;
-                const uint64_t S = P1t - r1[jj & RM];
-                const uint64_t Tq = (P2t - r2[jj & RM]) - (uint64_t)(int64_t)jj * S;
+                const int pj = ring_back(ptop, Wn, R);
+                const uint64_t S = P1t - r1[pj];
+                const uint64_t Tq = (P2t - r2[pj]) - (uint64_t)(int64_t)jj * S;
                 const int64_t N = (int64_t)(2 * Tq - (uint64_t)(Wn - 1) * S);
                 const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
                 if (lane == 0) {
@@ -367,7 +382,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          const int32_t* __restrict__ close,
                                                          Grid g, Out out, int nextra) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nw = g.na, nk = g.nb, R = g.ring, RM = g.ring - 1;
+    const int nw = g.na, nk = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(1, R, nw, nk);
     uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);                    // sum c
     unsigned __int128* r2 = reinterpret_cast<unsigned __int128*>(smem + LL.r2);  // sum c^2
@@ -418,13 +433,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
-        r1[(t + 1) & RM] = (uint64_t)pre;
+        const int pt = ring_pos(T, lane, R);
+        r1[pt] = (uint64_t)pre;
         // sum of c^2 in 128 bits: scan the 32-bit halves of c^2 < 2^62 separately
         const uint64_t c2 = (uint64_t)((int64_t)c * c);
         const int64_t slo = wave_iscan_i64((int64_t)(c2 & 0xFFFFFFFFu));
         const int64_t shi = wave_iscan_i64((int64_t)(c2 >> 32));
         const unsigned __int128 inc2 = ((unsigned __int128)(uint64_t)shi << 32) + (uint64_t)slo;
-        r2[(t + 1) & RM] = cy2 + inc2;
+        r2[pt] = cy2 + inc2;
         cy2 += ((unsigned __int128)(uint64_t)lane63_i64(shi) << 32) + (uint64_t)lane63_i64(slo);
         // raw lows / highs and their 8-bar block extrema
         int32_t* LH = lhs_ + s * kLH;
@@ -447,8 +463,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int s = T % kTileStages, t = T * kTile + lane;
         const int64_t c = cts[s * kTile + lane];
         uint64_t* Wd = words + (T & 1) * nword;
-        const uint64_t P1t = r1[(t + 1) & RM];
-        const unsigned __int128 P2t = r2[(t + 1) & RM];
+        const int ptop = ring_pos(T, lane, R);
+        const uint64_t P1t = r1[ptop];
+        const unsigned __int128 P2t = r2[ptop];
         const uint32_t base = (uint32_t)T * (uint32_t)(nw + nwaves);
         uint32_t o = grab_task(ctr, lane) - base;
 #pragma unroll 1
@@ -457,8 +474,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int Wn = win[o];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
-            const int64_t S1 = (int64_t)(P1t - r1[jj & RM]);
-            const unsigned __int128 S2 = P2t - r2[jj & RM];
+            const int pj = ring_back(ptop, Wn, R);
+            const int64_t S1 = (int64_t)(P1t - r1[pj]);
+            const unsigned __int128 S2 = P2t - r2[pj];
             const int64_t Dv = (int64_t)Wn * c - S1;
             const i128 Q = (i128)Wn * (i128)S2 - (i128)S1 * (i128)S1;  // >= 0 on valid bars
             // fp64 fast path: |z| > k <=> Dv^2 kd^2 > kn^2 Q, both sides within 2^-50 relative

@@ -268,3 +268,27 @@ def test_sma_block_shapes(nf, ns):
     for s in range(S):
         for p in range(grid.n_params):
             compare_summary(got[s, p], orc[s, p], f"shape {nf}x{ns} sym {s} param {p}")
+
+
+@pytest.mark.parametrize("strategy", ["sma", "ema_ols", "boll"])
+def test_spec_maximum_windows(strategy):
+    """Windows up to the spec's 4,096 bars (docs/oracle_spec.md §3: w <= 4096 keeps window
+    sums < 2^43), beside short ones, on 12,000-bar series: prefix rings of ~4.3k entries."""
+    if strategy == "sma":
+        grid = D.Grid.sma([3, 500], [4096, 700], annualization=98280)
+    elif strategy == "ema_ols":
+        grid = D.Grid.ema_ols([5, 4000], [4096, 16], band_bps=20)
+    else:
+        grid = D.Grid.boll([4096, 12], [2, 5], [50], [100, 400], k_den=2)
+    bars = 12000
+    o, h, lo, c = _gen(0x5EED, [8, 9], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 8, 2, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(2):
+        orc, otr = oracle_row(strategy, grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} max windows sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
