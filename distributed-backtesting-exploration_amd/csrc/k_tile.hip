@@ -403,10 +403,15 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
     const int j = blockIdx.y * npw * 64 + tid;
     const bool active = wave < npw && j < P;
-    const int pj = active ? j : 0;
-    // param = ((iw * nk + ik) * nsl + isl) * ntp + itp
-    const int itp = pj % g.nd, isl = (pj / g.nd) % g.nc, ik = (pj / (g.nd * g.nc)) % nk,
-              iw = pj / (g.nd * g.nc * nk);
+    // lanes run k-major (lane j -> (ik, iw, isl, itp)) while results keep the param order
+    // ((iw * nk + ik) * nsl + isl) * ntp + itp: a wave then holds one z threshold, and the
+    // threshold sets most of a lane's trade rate, so the walk (a wave iterates the maximum
+    // over its lanes' trades per tile) wastes fewer lanes: 20.2 -> 17.8 iterations per
+    // block-tile on config 4 (oracle trade lists of 3 symbols)
+    const int jl = active ? j : 0;
+    const int itp = jl % g.nd, isl = (jl / g.nd) % g.nc, iw = (jl / (g.nd * g.nc)) % nw,
+              ik = jl / (g.nd * g.nc * nw);
+    const int pj = ((iw * nk + ik) * g.nc + isl) * g.nd + itp;
     const int w = g.a[iw];
     const int32_t sl_bps = g.c[isl], tp_bps = g.d[itp];
     const int32_t* crow = close + sd.off;
