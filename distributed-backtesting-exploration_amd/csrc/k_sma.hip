@@ -32,6 +32,7 @@ namespace {
 
 constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned for b128 reads
 constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
+constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
 
 struct SmaLds {                       // byte offsets into dynamic LDS
     size_t ring, keys, invw, win, dst, ct, ql, ctr, total;
@@ -43,8 +44,8 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
     L.ring = take((size_t)ring * 8);
     L.keys = take((size_t)2 * nw * kKS * 4);
-    L.invw = take((size_t)(nw + 1) * 8);   // + pad: window pairs are read as one 16-B load
-    L.win = take((size_t)(nw + 1) * 4);
+    L.invw = take((size_t)(nw + kKeyGrab) * 8);   // + pad: key groups read whole 16-B words
+    L.win = take((size_t)(nw + kKeyGrab) * 4);
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
@@ -108,18 +109,19 @@ __device__ __forceinline__ void stage_scan(int32_t c, int B, int t0, int lane, i
 
 // Stage 2 for one tile: int32 floor keys for every window. lane = bar, so the window length
 // and its reciprocal are wave-uniform and the top of the ring is read once per tile.
-// Windows are handed out dynamically, two per grab: every wave of the block (helper included)
-// grabs window pairs from an LDS counter after its other work for the tile, so waves with few
-// flips to walk compute more keys. Round r owns counter values [r*per, (r+1)*per) with
-// per = 2*ceil(nw/2) + 2*nwaves: the pair grabs plus exactly one failing grab per wave (the
-// barrier separates rounds). The next pair's atomic is in flight while the current pair
-// computes (its result is read only at the end of the iteration).
+// Windows are handed out dynamically, kKeyGrab per grab: every wave of the block (helper
+// included) grabs window groups from an LDS counter after its other work for the tile, so waves
+// with few flips to walk compute more keys. Round r owns counter values [r*per, (r+1)*per) with
+// per = kKeyGrab * (ceil(nw / kKeyGrab) + nwaves): the group grabs plus exactly one failing grab
+// per wave (the barrier separates rounds). The next group's atomic is in flight while the
+// current group computes (its result is read only at the end of the iteration), and the group's
+// ring reads are issued together.
 // Bars without a full window (or past the series end) get key -1 on fast rows and -2 on slow
 // rows: their difference is never 0, so they never look like ties to the compare stage (they
 // are outside every lane's decision mask anyway).
 __device__ __forceinline__ uint32_t grab_issue(uint32_t* ctr, int lane) {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(ctr, 2u);
+    if (lane == 0) v = atomicAdd(ctr, (uint32_t)kKeyGrab);
     return v;
 }
 
@@ -140,26 +142,38 @@ __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R,
     const int t = t0 + lane;
     const double top = ring[(t + 1) & (R - 1)];
     const bool tin = t < B;
-    const uint32_t per = 2u * (uint32_t)((nw + 1) >> 1) + 2u * (uint32_t)nwaves;
+    const uint32_t per = (uint32_t)kKeyGrab * ((uint32_t)(nw + kKeyGrab - 1) / kKeyGrab + nwaves);
     const uint32_t base = round * per;
     uint32_t w = __builtin_amdgcn_readlane(grab_issue(ctr, lane), 0) - base;
 #pragma unroll 1
     while (w < (uint32_t)nw) {
-        const uint32_t vn = grab_issue(ctr, lane);  // next pair, read at the end
-        // w is even: win[w..w+1] and invw[w..w+1] are one aligned 8-B / 16-B read each (the
-        // LDS regions are padded, so w + 1 == nw reads a pad entry that is never used)
-        const int2 W2 = *reinterpret_cast<const int2*>(win + w);
-        const double2 I2 = *reinterpret_cast<const double2*>(invw + w);
-        const int W0 = __builtin_amdgcn_readfirstlane(W2.x);
-        const bool two = w + 1 < (uint32_t)nw;
-        const int W1 = two ? __builtin_amdgcn_readfirstlane(W2.y) : W0;
-        const double F0 = top - ring[(t + 1 - W0) & (R - 1)];  // exact (< 2^53)
-        const double F1 = top - ring[(t + 1 - W1) & (R - 1)];
-        const int32_t k0 = floor_key(F0, W0, I2.x);
-        K[w * kKS + lane] = (tin && t + 1 - W0 >= 0) ? k0 : ((int)w < nf ? -1 : -2);
-        if (two) {
-            const int32_t k1 = floor_key(F1, W1, I2.y);
-            K[(w + 1) * kKS + lane] = (tin && t + 1 - W1 >= 0) ? k1 : ((int)w + 1 < nf ? -1 : -2);
+        const uint32_t vn = grab_issue(ctr, lane);  // next group, read at the end
+        // w is a multiple of kKeyGrab: the group's lengths and reciprocals are aligned 16-B
+        // reads (the LDS regions are padded; entries past nw are never used)
+        int Wv[kKeyGrab];
+        double Iv[kKeyGrab], Fv[kKeyGrab];
+#pragma unroll
+        for (int q = 0; q < kKeyGrab; q += 4) {
+            const int4 W4 = *reinterpret_cast<const int4*>(win + w + q);
+            Wv[q] = W4.x; Wv[q + 1] = W4.y; Wv[q + 2] = W4.z; Wv[q + 3] = W4.w;
+        }
+#pragma unroll
+        for (int q = 0; q < kKeyGrab; q += 2) {
+            const double2 I2 = *reinterpret_cast<const double2*>(invw + w + q);
+            Iv[q] = I2.x; Iv[q + 1] = I2.y;
+        }
+#pragma unroll
+        for (int q = 0; q < kKeyGrab; ++q) {
+            Wv[q] = __builtin_amdgcn_readfirstlane(w + q < (uint32_t)nw ? Wv[q] : Wv[0]);
+            Fv[q] = top - ring[(t + 1 - Wv[q]) & (R - 1)];  // exact (< 2^53)
+        }
+#pragma unroll
+        for (int q = 0; q < kKeyGrab; ++q) {
+            if (w + q < (uint32_t)nw) {
+                const int32_t kq = floor_key(Fv[q], Wv[q], Iv[q]);
+                K[(w + q) * kKS + lane] =
+                    (tin && t + 1 - Wv[q] >= 0) ? kq : ((int)(w + q) < nf ? -1 : -2);
+            }
         }
         w = __builtin_amdgcn_readlane(vn, 0) - base;
     }
