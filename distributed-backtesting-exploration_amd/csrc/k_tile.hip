@@ -66,13 +66,16 @@ __device__ __forceinline__ int32_t ldc(const int32_t* __restrict__ row, int B, i
     return t < B ? row[t] : pad;
 }
 
-// Window task counter: round r owns counter values [r * (n + nwaves), (r + 1) * (n + nwaves)):
+// Task counter: round r owns counter values [r * (n + nwaves), (r + 1) * (n + nwaves)):
 // n successful grabs plus exactly one failing grab per wave (the barrier separates rounds).
-__device__ __forceinline__ uint32_t grab_task(uint32_t* ctr, int lane) {
+// grab_issue returns the atomic's VGPR; the caller reads lane 0 only when it needs the value,
+// so the next grab's round trip overlaps the current task.
+__device__ __forceinline__ uint32_t grab_issue(uint32_t* ctr, int lane) {
     uint32_t v = 0;
     if (lane == 0) v = atomicAdd(ctr, 1u);
-    return __builtin_amdgcn_readlane(v, 0);
+    return v;
 }
+__device__ __forceinline__ uint32_t grab_value(uint32_t v) { return __builtin_amdgcn_readlane(v, 0); }
 
 // Prefix rings: entry x (the sum over bars < x) lives at x mod R, with R a multiple of 64 of at
 // least the longest window + 3 tiles (engine.cpp), so windows up to the spec's 4,096 bars fit
@@ -192,10 +195,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const int ptop = ring_pos(T, lane, R);
         const uint64_t P1t = r1[ptop], P2t = r2[ptop];
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + nwaves);
-        uint32_t o = grab_task(ctr, lane) - base;
+        uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
         while (o < (uint32_t)ntask) {
-            const uint32_t nxt = grab_task(ctr, lane) - base;
+            const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
             if ((int)o < nsp) {  // span: entry / exit conditions against the EMA
                 const double e = E[o * kEStride + lane];
                 const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     Wd[4 * nsp + 2 * ow + 1] = wn;
                 }
             }
-            o = nxt;
+            o = grab_value(vn) - base;
         }
     };
 
@@ -472,10 +475,10 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const uint64_t P1t = r1[ptop];
         const unsigned __int128 P2t = r2[ptop];
         const uint32_t base = (uint32_t)T * (uint32_t)(nw + nwaves);
-        uint32_t o = grab_task(ctr, lane) - base;
+        uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
         while (o < (uint32_t)nw) {
-            const uint32_t nxt = grab_task(ctr, lane) - base;
+            const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
             const int Wn = win[o];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 Wd[2 * nw * nk + 2 * o] = dp;
                 Wd[2 * nw * nk + 2 * o + 1] = dn;
             }
-            o = nxt;
+            o = grab_value(vn) - base;
         }
     };
 
