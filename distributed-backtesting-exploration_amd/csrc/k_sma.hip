@@ -71,9 +71,11 @@ __device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, 
 }
 
 // c = close of bar t0 + lane (0 past the end), loaded one tile ahead by the caller so the HBM
-// latency is off the pipeline's critical path.
-__device__ __forceinline__ void stage_scan(int32_t c, int B, int t0, int lane, int R, double* ring,
-                                           int32_t* cT, int64_t* ql, Agg* D, ScanCarry& cy) {
+// latency is off the pipeline's critical path. Stage 1 is split over two waves: stage_ring
+// (prefix ring, closes, return prefixes) on the last wave and stage_dst (the drawdown table)
+// on the one before it, each from its own copy of the tile's closes.
+__device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, int R, double* ring,
+                                           int32_t* cT, int64_t* ql, ScanCarry& cy) {
     const int t = t0 + lane;
     const bool valid = t < B;
     // previous bar's close: DPP wave_shr:1, lane 0 takes the carry
@@ -88,8 +90,11 @@ __device__ __forceinline__ void stage_scan(int32_t c, int B, int t0, int lane, i
     ql[kTile + lane] = wave_iscan_i64(q2);
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
-    // DST by doubling: S_m / P_m = aggregate from the bar to the end / from the start of its
-    // aligned 2^m block. Level L of the DST is S_L on left halves and P_L on right halves.
+}
+
+// DST by doubling: S_m / P_m = aggregate from the bar to the end / from the start of its
+// aligned 2^m block. Level L of the DST is S_L on left halves and P_L on right halves.
+__device__ __forceinline__ void stage_dst(int32_t c, int lane, Agg* D) {
     Agg S = agg_one(c), Pp = S;
     D[lane] = S;  // level 0
 #pragma unroll
@@ -295,6 +300,11 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
     // otherwise (a grid that fills all 16 waves of one block) it also walks 64 parameters
     const int nwaves = (int)blockDim.x >> 6;
     const bool helper = (tid >> 6) == nwaves - 1;
+    // the wave before it builds the drawdown tables (stage_dst); profiling bit 16 keeps both
+    // parts of stage 1 on the last wave
+    const bool split = !(g.ablate & 16);
+    const bool dstw = split && (tid >> 6) == nwaves - 2;
+    const bool dsth = helper && !split;
     const int nparam_threads = dedicated ? (int)blockDim.x - 64 : (int)blockDim.x;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
@@ -328,14 +338,16 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
     // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0. The helper keeps the closes of the
     // tile after next in flight (cpre) across the barrier.
     int32_t cpre = 0;
-    if (helper) {
+    if (helper || dstw) {
         const int32_t c0 = load_close(crow, B, lane), c1 = load_close(crow, B, kTile + lane);
         cpre = load_close(crow, B, 2 * kTile + lane);
-        stage_scan(c0, B, 0, lane, R, ring, cts, qls, dst, cy);
+        if (helper) stage_ring(c0, B, 0, lane, R, ring, cts, qls, cy);
+        if (dstw || dsth) stage_dst(c0, lane, dst);
         __syncthreads();
-        if (ntiles > 1)
-            stage_scan(c1, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile,
-                       dst + kDstLevels * kTile, cy);
+        if (ntiles > 1) {
+            if (helper) stage_ring(c1, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile, cy);
+            if (dstw || dsth) stage_dst(c1, lane, dst + kDstLevels * kTile);
+        }
     } else {
         __syncthreads();
     }
@@ -370,10 +382,12 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
         const int t0 = k * kTile;
         // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
         // (tile k+1) on every wave, balanced dynamically
-        if (helper && k + 2 < ntiles && !(g.ablate & 1)) {
+        if ((helper || dstw) && k + 2 < ntiles && !(g.ablate & 1)) {
             const int s = (k + 2) % kStages;
-            stage_scan(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
-                       qls + s * 2 * kTile, dst + s * kDstLevels * kTile, cy);
+            if (helper)
+                stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+                           qls + s * 2 * kTile, cy);
+            if (dstw || dsth) stage_dst(cpre, lane, dst + s * kDstLevels * kTile);
             cpre = load_close(crow, B, t0 + 3 * kTile + lane);
         }
         BT_STAMP(0)
