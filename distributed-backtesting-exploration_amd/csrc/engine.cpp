@@ -91,7 +91,8 @@ struct bt_engine {
     DevBuf<unsigned int> d_hist, d_counts;
     DevBuf<unsigned long long> d_state, d_above, d_cand;
     DevBuf<bt_topk_rec> d_top;
-    DevBuf<int32_t> d_topn;
+    bt_topk_rec* h_top = nullptr;     // pinned host copy of d_top
+    bool topk_ready = false;          // top-k buffers allocated and their state initialised
     bool ran = false;
     // timing of the dominant kernel
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
@@ -228,6 +229,11 @@ void layout(bt_engine* e, int32_t n_sym, const int32_t* bars, const int64_t* ids
     e->ran = false;
 }
 
+TopkWork topk_work(bt_engine* e) {
+    return TopkWork{e->d_hist.p, e->d_state.p, e->d_counts.p, e->d_above.p, e->d_cand.p,
+                    kTopkCap, e->d_top.p + 1, reinterpret_cast<int32_t*>(e->d_top.p)};
+}
+
 void ensure_outputs(bt_engine* e) {
     const size_t n = (size_t)e->syms.size() * e->P;
     e->d_sum.ensure(std::max<size_t>(1, n));
@@ -237,14 +243,16 @@ void ensure_outputs(bt_engine* e) {
         e->d_sums.ensure(std::max<size_t>(1, n));
         e->d_trades.ensure(std::max<size_t>(1, n * (size_t)e->cfg.trade_cap));
     }
-    if (e->cfg.topk > 0) {
+    if (e->cfg.topk > 0 && !e->topk_ready) {
         e->d_hist.ensure(4096);
         e->d_counts.ensure(2);
         e->d_state.ensure(4);
         e->d_above.ensure(kTopkCap);
         e->d_cand.ensure(kTopkCap);
-        e->d_top.ensure(kTopkMax);
-        e->d_topn.ensure(1);
+        e->d_top.ensure(kTopkMax + 1);  // [0] = header (record count), then the records
+        if (!e->h_top) HIPCHK(hipHostMalloc(&e->h_top, (kTopkMax + 1) * sizeof(bt_topk_rec)));
+        HIPCHK(launch_topk_init(topk_work(e), e->stream));
+        e->topk_ready = true;
     }
 }
 
@@ -298,10 +306,8 @@ void run_impl(bt_engine* e) {
         e->ev_pending.push_back(ev);
     }
     if (e->cfg.topk > 0) {
-        TopkWork w{e->d_hist.p, e->d_state.p, e->d_counts.p, e->d_above.p, e->d_cand.p,
-                   kTopkCap, e->d_top.p, e->d_topn.p};
         HIPCHK(launch_topk(e->d_key.p, e->d_sum.p, e->d_syms.p, (int64_t)S * e->P, e->P,
-                           e->cfg.topk, w, e->stream));
+                           e->cfg.topk, topk_work(e), e->stream));
     }
     e->ran = true;
 }
@@ -327,13 +333,16 @@ bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b) {  // "a ranks before
 
 std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
+    // header + the configured k records in one copy into pinned memory
+    const size_t nrec = (size_t)e->cfg.topk + 1;
+    HIPCHK(hipMemcpyAsync(e->h_top, e->d_top.p, nrec * sizeof(bt_topk_rec), hipMemcpyDeviceToHost,
+                          e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     int32_t n = 0;
-    HIPCHK(hipMemcpy(&n, e->d_topn.p, sizeof n, hipMemcpyDeviceToHost));
+    memcpy(&n, e->h_top, sizeof n);
     std::vector<bt_topk_rec> res;
     if (n >= 0) {
-        res.resize((size_t)n);
-        if (n) HIPCHK(hipMemcpy(res.data(), e->d_top.p, (size_t)n * sizeof(bt_topk_rec), hipMemcpyDeviceToHost));
+        res.assign(e->h_top + 1, e->h_top + 1 + n);
     } else {  // more than kTopkCap records tie on the selected prefix: finish on the host
         const size_t total = e->syms.size() * (size_t)e->P;
         std::vector<bt_summary> all(total);
@@ -484,7 +493,9 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_above.release();
         e->d_cand.release();
         e->d_top.release();
-        e->d_topn.release();
+        if (e->h_top) (void)hipHostFree(e->h_top);
+        e->h_top = nullptr;
+        e->topk_ready = false;
         if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     } catch (...) {
     }

@@ -80,6 +80,7 @@ struct TopkWork {
 };
 hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms,
                        int64_t n, int32_t P, int32_t k, const TopkWork& w, hipStream_t st);
+hipError_t launch_topk_init(const TopkWork& w, hipStream_t st);  // once per buffer allocation
 
 // Shared host/device helpers.
 __host__ __device__ inline uint64_t order_key(double x) {

@@ -438,7 +438,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     int32_t cpre = 0, hpre = 0, lpre = 0;
 
     auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
-        const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
+        const int s = T % kTileStages, t0 = T * kTile;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
         const int pt = ring_pos(T, lane, R);

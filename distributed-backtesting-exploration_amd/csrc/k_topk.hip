@@ -5,7 +5,7 @@
 //   -> collect: records whose 24-bit prefix is above the selected one (< k of them) and the
 //      candidates that share it -> finish: one block sorts them in LDS by
 //      (key desc, sym asc, param asc) and writes the k result records.
-// Seven small launches, no host round trip; the host reads one count and k records. The order
+// Seven small launches, no host round trip; the host reads the count and k records in one copy. The order
 // is exact and deterministic (atomics only decide collection order, which the sort removes).
 // If more than kCap records tie on the 24-bit prefix, finish reports overflow (-1) and the
 // host completes the selection from the raw keys.
@@ -36,40 +36,51 @@ __global__ __launch_bounds__(256) void topk_hist(const uint64_t* __restrict__ ke
 }
 
 // One block of 256 threads; thread t owns bins 4095-16t .. 4080-16t (counted from the top).
+// The owner of the k-th record is found by a block scan of the 256 partial sums; it resolves
+// the bin from its own 16 counts. `need0` > 0 on the first digit (state[2] is set from it).
 __global__ __launch_bounds__(256) void topk_select(unsigned int* __restrict__ hist, int shift,
-                                                   unsigned long long* __restrict__ state) {
-    __shared__ unsigned int part[256];
+                                                   unsigned long long* __restrict__ state,
+                                                   unsigned long long need0) {
+    __shared__ unsigned long long part[256];
     const int t = threadIdx.x;
     const int top = kBins - 1 - 16 * t;
-    unsigned int s = 0;
-    for (int j = 0; j < 16; ++j) s += hist[top - j];
+    unsigned int c[16];
+    unsigned long long s = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        c[j] = hist[top - j];
+        s += c[j];
+    }
     part[t] = s;
     __syncthreads();
-    if (t == 0) {
-        const unsigned long long need = state[2];
-        unsigned long long cum = 0;
-        int owner = 255;
-        for (int i = 0; i < 256; ++i) {
-            if (cum + part[i] >= need) {
-                owner = i;
-                break;
-            }
-            cum += part[i];
-        }
-        const int b = kBins - 1 - 16 * owner;
-        int bin = b - 15;
+    // inclusive Hillis-Steele scan over the 256 partial sums (bins from the top)
+    for (int d = 1; d < 256; d <<= 1) {
+        const unsigned long long v = t >= d ? part[t - d] : 0ULL;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const unsigned long long need = need0 ? need0 : state[2];
+    const unsigned long long incl = part[t], excl = incl - s;
+    // owner: the first group whose inclusive count reaches `need` (the last group if the
+    // histogram holds fewer records than need: then every record is taken)
+    const bool owner = (excl < need && incl >= need) || (t == 255 && incl < need);
+    __syncthreads();
+    if (owner) {
+        unsigned long long cum = excl;
+        int bin = top - 15;
+#pragma unroll
         for (int j = 0; j < 16; ++j) {
-            if (cum + hist[b - j] >= need) {
-                bin = b - j;
+            if (cum + c[j] >= need) {
+                bin = top - j;
                 break;
             }
-            cum += hist[b - j];
+            cum += c[j];
         }
         state[0] |= (unsigned long long)bin << shift;
         state[1] |= (unsigned long long)(kBins - 1) << shift;
         state[2] = need - cum;
     }
-    __syncthreads();
     for (int i = t; i < kBins; i += blockDim.x) hist[i] = 0;  // ready for the next digit
 }
 
@@ -154,32 +165,45 @@ __global__ __launch_bounds__(1024) void topk_finish(
     if (threadIdx.x == 0) out_n[0] = take;
 }
 
-__global__ void topk_init(unsigned long long* state, unsigned int* counts, unsigned int* hist,
-                          unsigned long long need) {
-    for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[i] = 0;
+// Reset the selection state for the next run (the histogram is left zeroed by topk_select).
+__global__ void topk_reset(unsigned long long* state, unsigned int* counts) {
     if (threadIdx.x == 0) {
-        state[0] = state[1] = 0;
-        state[2] = need;
+        state[0] = state[1] = state[2] = 0;
         counts[0] = counts[1] = 0;
     }
 }
 
+__global__ void topk_init(unsigned long long* state, unsigned int* counts, unsigned int* hist) {
+    for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[i] = 0;
+    if (threadIdx.x == 0) {
+        state[0] = state[1] = state[2] = 0;
+        counts[0] = counts[1] = 0;
+    }
+}
+
+hipError_t launch_topk_init(const TopkWork& w, hipStream_t st) {
+    hipLaunchKernelGGL(topk_init, dim3(1), dim3(256), 0, st, w.state, w.counts, w.hist);
+    return hipGetLastError();
+}
+
+// The chain assumes the state left by topk_init or by the previous chain's topk_reset.
 hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms, int64_t n,
                        int32_t P, int32_t k, const TopkWork& w, hipStream_t st) {
     if (n <= 0 || k <= 0) return hipSuccess;
     const unsigned long long need = (unsigned long long)(k < n ? k : n);
     int64_t blocks = (n + 2047) / 2048;
     if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(topk_init, dim3(1), dim3(256), 0, st, w.state, w.counts, w.hist, need);
     for (int shift = 52; shift >= 40; shift -= 12) {
         hipLaunchKernelGGL(topk_hist, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
                            (const unsigned long long*)w.state, w.hist);
-        hipLaunchKernelGGL(topk_select, dim3(1), dim3(256), 0, st, w.hist, shift, w.state);
+        hipLaunchKernelGGL(topk_select, dim3(1), dim3(256), 0, st, w.hist, shift, w.state,
+                           shift == 52 ? need : 0ULL);
     }
     hipLaunchKernelGGL(topk_collect, dim3((unsigned)blocks), dim3(256), 0, st, key, n,
                        (const unsigned long long*)w.state, w.counts, w.above, w.cand, w.cap);
     hipLaunchKernelGGL(topk_finish, dim3(1), dim3(1024), (size_t)w.cap * 24, st, key, sum, syms,
                        P, w.counts, w.above, w.cand, w.cap, k, w.out, w.out_n);
+    hipLaunchKernelGGL(topk_reset, dim3(1), dim3(64), 0, st, w.state, w.counts);
     return hipGetLastError();
 }
 
