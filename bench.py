@@ -1,14 +1,18 @@
 """bench.py — bar-evals/s of the backtest hot path on 1..N MI355X (BASELINE.json metric).
 
-Workload (N=1 and per GPU for N>1): BASELINE config 2 — SMA fast/slow crossover,
+Default workload (N=1 and per GPU for N>1): BASELINE config 2 — SMA fast/slow crossover,
 5,000 symbols x 2,520 daily bars x 400 param pairs, synthetic OHLC (docs/oracle_spec.md §1)
 generated directly in HBM before timing. One step = one pass of the hot path over that batch:
-the fused SMA kernel (indicators + signals + position/PnL/drawdown/Sharpe per lane) and the
+the fused strategy kernel (indicators + signals + position/PnL/drawdown/Sharpe per lane) and the
 per-GPU top-k; for N>1 also the RCCL all-gather of the top-k records + all-reduce of counters
 (the only exchange step). Symbols are sharded across ranks with no data-path
-collective (weak scaling: every rank runs its own 5,000 symbols).
+collective (weak scaling: every rank runs its own shard).
 
-Run: python bench.py [--gpus N --steps K --warmup W]
+`--config 3|4|5` measures the per-GPU shard of the other BASELINE configs the same way (EMA+OLS
+500 x 98,280 x 64; Bollinger 500 x 98,280 x 256, i.e. 2,000 symbols over 4 GPUs; SMA
+1,250 x 491,400 x 1,024, i.e. 10,000 symbols over 8 GPUs); the driver runs the default.
+
+Run: python bench.py [--gpus N --steps K --warmup W] [--config C]
      torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 from __future__ import annotations
@@ -27,8 +31,21 @@ import numpy as np  # noqa: E402
 import dbx_amd as D  # noqa: E402
 from dbx_amd import parallel as PAR  # noqa: E402
 
-S_PER_GPU, BARS, SEED, TOPK = 5000, 2520, 0x5EED, 100
+SEED, TOPK = 0x5EED, 100
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# per-GPU shard of each BASELINE config: grid, symbols, bars, bar frequency, annualization,
+# and the SURVEY.md §8(d) byte-model terms c (OHLC columns consumed) and W (indicator series)
+CONFIGS = {
+    2: dict(grid=D.config2_grid, S=5000, B=2520, freq=D.BT_DAILY, ann=252, c=1, W=40,
+            name="BASELINE config 2: SMA fast/slow crossover"),
+    3: dict(grid=D.config3_grid, S=500, B=98280, freq=D.BT_MINUTE, ann=98280, c=1, W=16,
+            name="BASELINE config 3: EMA + rolling-OLS-slope mean reversion"),
+    4: dict(grid=D.config4_grid, S=500, B=98280, freq=D.BT_MINUTE, ann=98280, c=3, W=16,
+            name="BASELINE config 4: Bollinger z-score with SL/TP (2,000 symbols over 4 GPUs)"),
+    5: dict(grid=D.config5_grid, S=1250, B=491400, freq=D.BT_MINUTE, ann=98280, c=1, W=64,
+            name="BASELINE config 5: SMA 32x32 grid, 5y 1-min bars (10,000 symbols over 8 GPUs)"),
+}
 
 
 def algorithmic_bytes(S, B, P, c=1, W=40):
@@ -36,42 +53,62 @@ def algorithmic_bytes(S, B, P, c=1, W=40):
     return S * B * (8 * c + 16 * W) + 32 * S * P
 
 
-def cpu_baseline(grid, threads=None, target_cpu_s=15.0):
-    """The C oracle (scalar, multithreaded: SURVEY B4) on a bounded sample of the same workload:
-    a 64-symbol probe sizes the sample to ~target_cpu_s thread-seconds (at most all 5,000)."""
+def cpu_baseline(cfg, grid, threads=None, target_thread_s=15.0):
+    """The C oracle (oracle/oracle.c, -O2 -ffp-contract=off) on the first symbols of
+    the same workload, sized from a one-symbol probe to ~target_thread_s thread-seconds. SMA
+    grids run on the oracle's pthread grid (one symbol per thread); EMA/Bollinger run one
+    (symbol, param) call per task on a thread pool (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc_ffi as F
     threads = threads or min(16, os.cpu_count() or 1)
-    fast, slow = np.asarray(grid.axes[0]), np.asarray(grid.axes[1])
+    B, freq, ann = cfg["B"], 1 if cfg["freq"] == D.BT_MINUTE else 0, cfg["ann"]
 
-    def timed(n):
-        closes = np.stack([F.gen(SEED, s, BARS, 0)[3] for s in range(n)])
+    def run(n):
+        cols = [F.gen(SEED, s, B, freq) for s in range(n)]
         t0 = time.perf_counter()
-        F.sma_grid_mt(closes, fast, slow, 252, threads)
+        if grid.strategy == D.BT_SMA_CROSS:
+            F.sma_grid_mt(np.stack([x[3] for x in cols]), np.asarray(grid.axes[0]),
+                          np.asarray(grid.axes[1]), ann, threads)
+        else:
+            def one(sp):
+                s, p = sp
+                o, h, lo, c = cols[s][:4]
+                kw = grid.param(p)
+                if grid.strategy == D.BT_EMA_OLS:
+                    F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], ann)
+                else:
+                    F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], ann)
+            with ThreadPoolExecutor(threads) as ex:
+                list(ex.map(one, [(s, p) for s in range(n) for p in range(grid.n_params)]))
         return time.perf_counter() - t0
 
-    probe = 64
-    dt = timed(probe)
-    n_sym = int(min(S_PER_GPU, max(probe, probe * target_cpu_s / threads / max(dt, 1e-6))))
+    probe = min(threads, cfg["S"]) if grid.strategy == D.BT_SMA_CROSS else 1
+    dt = run(probe)
+    thread_s = dt * (threads if grid.strategy != D.BT_SMA_CROSS else min(threads, probe))
+    per_sym = thread_s / probe
+    n_sym = int(min(cfg["S"], max(probe, target_thread_s / max(per_sym, 1e-9))))
     if n_sym > probe:
-        dt = timed(n_sym)
+        dt = run(n_sym)
     else:
         n_sym = probe
-    evals = n_sym * BARS * grid.n_params
+    evals = n_sym * B * grid.n_params
     return {"value": evals / dt, "unit": "bar-evals/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_sym} of the 5000 config-2 symbols x {BARS} bars x "
+            "sample": f"first {n_sym} of the {cfg['S']} shard symbols x {B} bars x "
                       f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall on "
-                      f"{threads} threads = {dt * threads:.1f} thread-s; oracle/oracle.c "
-                      f"orc_sma_grid_mt, gcc -O2 -ffp-contract=off)"}
+                      f"{threads} threads; oracle/oracle.c, gcc -O2 -ffp-contract=off)"}
 
 
-def load_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_sma_config2.json")
-    if not os.path.exists(path):
-        return None
+def load_traffic(config):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries."""
+    path = os.path.join(ROOT, "profiles", "pmc_sma_config2.json") if config == 2 else \
+        os.path.join(ROOT, "profiles", "r01_configs", "configs.json")
     try:
-        return float(json.load(open(path))["hbm_bytes_per_launch"])
+        d = json.load(open(path))
+        if config == 2:
+            return float(d["hbm_bytes_per_launch"])
+        v = d[f"config{config}"]
+        return float(v["hbm_read_bytes"] + v["hbm_write_bytes"])
     except Exception:
         return None
 
@@ -81,8 +118,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    S_PER_GPU, BARS = cfg["S"], cfg["B"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,10 +143,10 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    grid = D.config2_grid()
+    grid = cfg["grid"]()
     P = grid.n_params
     eng = D.Engine(grid, device=device, topk=TOPK, timing=True)
-    eng.load_synthetic(SEED, rank * S_PER_GPU, S_PER_GPU, BARS, D.BT_DAILY)
+    eng.load_synthetic(SEED, rank * S_PER_GPU, S_PER_GPU, BARS, cfg["freq"])
 
     def step():
         eng.run()
@@ -146,9 +186,9 @@ def main():
         evals_per_step = S_PER_GPU * BARS * P * world
         value = evals_per_step * args.steps / elapsed
         kavg_s = kms / 1e3 / max(launches, 1)
-        alg = algorithmic_bytes(S_PER_GPU, BARS, P)
+        alg = algorithmic_bytes(S_PER_GPU, BARS, P, cfg["c"], cfg["W"])
         achieved = alg / kavg_s / 1e9
-        traffic = load_traffic()
+        traffic = load_traffic(args.config)
         line = {
             "metric": "bar-evals/sec (symbols x params x bars)",
             "value": value,
@@ -162,7 +202,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64+int64",
             "data": "synthetic (SplitMix64 integer OHLC walk, docs/oracle_spec.md §1, generated in HBM)",
-            "config": {"workload": "BASELINE config 2: SMA fast/slow crossover",
+            "config": {"workload": cfg["name"],
                        "symbols_per_gpu": S_PER_GPU, "bars": BARS, "params": P,
                        "topk": TOPK, "parallelism": f"dp{world} (symbol shards, "
                        f"{'RCCL' if dist is None or dist.get_backend() == 'nccl' else 'gloo'} top-k gather)"},
@@ -176,7 +216,7 @@ def main():
                      "param": int(top[0]["param"])} if len(top) else None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(grid)
+            line["cpu_baseline"] = cpu_baseline(cfg, grid)
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:

@@ -12,7 +12,7 @@ fi
 timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_quick.log 2>&1 || exit $?
 cut -c1-420 gpurun_out/bench_quick.log
 for c in $CFGS; do
-  timeout -k 10 240 python -u scripts/bench_configs.py --config $c > gpurun_out/cfg$c.log 2>&1 || { cat gpurun_out/cfg$c.log | tail -5; exit 1; }
+  timeout -k 10 240 python -u bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/cfg$c.log 2>&1 || { cat gpurun_out/cfg$c.log | tail -5; exit 1; }
   cut -c1-400 gpurun_out/cfg$c.log
 done
 exit 0

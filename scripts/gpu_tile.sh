@@ -7,5 +7,5 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 tail -4 gpurun_out/pt.log | cut -c1-600; [ $rc -ne 0 ] && exit $rc
 for c in $CFGS; do
   timeout -k 10 120 python -u scripts/stamps_tile.py $c || exit 1
-  timeout -k 10 120 python -u scripts/bench_configs.py --config $c | cut -c1-300 || exit 1
+  timeout -k 10 120 python -u bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline | cut -c1-300 || exit 1
 done
