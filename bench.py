@@ -153,9 +153,9 @@ def main():
         top = eng.read_topk()          # syncs the engine stream
         if dist is None:
             return top
-        # the one exchange step: RCCL all-gather of k x 24 B per rank + counter all-reduce
-        top = PAR.gather_topk(top, TOPK, dist)
-        PAR.allreduce_counters([S_PER_GPU * BARS * P, eng.stats()["trades"]], dist)
+        # the one exchange step: a single RCCL all-gather carrying each rank's k x 24 B top-k
+        # records and its run counters (summed on the host)
+        top, _ = PAR.exchange(top, TOPK, [S_PER_GPU * BARS * P, eng.stats()["trades"]], dist)
         return top
 
     for _ in range(args.warmup):

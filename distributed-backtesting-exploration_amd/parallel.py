@@ -46,6 +46,28 @@ def gather_topk(local: np.ndarray, k: int, dist) -> np.ndarray:
     return merge_topk(np.concatenate(parts) if parts else np.zeros(0, TOPK_DTYPE), k)
 
 
+def exchange(local: np.ndarray, k: int, counters, dist) -> tuple:
+    """The whole per-step exchange as ONE all-gather: each rank contributes
+    [k records (3 int64 words each) | record count | counters...], so the top-k merge and the
+    counter sum need a single latency-bound collective over xGMI instead of three.
+    Returns (merged top-k, summed counters)."""
+    import torch
+    world = dist.get_world_size()
+    nc = len(counters)
+    buf = np.zeros(3 * k + 1 + nc, np.int64)
+    n = min(len(local), k)
+    buf[:3 * n] = np.asarray(local, TOPK_DTYPE)[:n].view(np.int64)
+    buf[3 * k] = n
+    buf[3 * k + 1:] = [int(v) for v in counters]
+    t = torch.from_numpy(buf).to(_device_for(dist))
+    out = torch.empty(world * buf.size, dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    g = out.cpu().numpy().reshape(world, buf.size)
+    parts = [g[r, :3 * int(g[r, 3 * k])].view(TOPK_DTYPE) for r in range(world)]
+    top = merge_topk(np.concatenate(parts) if parts else np.zeros(0, TOPK_DTYPE), k)
+    return top, [int(x) for x in g[:, 3 * k + 1:].sum(axis=0)]
+
+
 def allreduce_counters(values, dist) -> list:
     """Sum int64 run counters (bar-evals, trades, errors) over all ranks."""
     import torch

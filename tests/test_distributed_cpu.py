@@ -43,6 +43,9 @@ def _worker(rank, world, port, q):
         local_top = D.merge_topk(local, K)
         top = PAR.gather_topk(local_top, K, dist)
         tot = PAR.allreduce_counters([count, len(local)], dist)
+        # bench.py's single-collective form: same merge, same sums
+        top2, tot2 = PAR.exchange(local_top, K, [count, len(local)], dist)
+        assert top2.tolist() == top.tolist() and tot2 == tot
         q.put((rank, top.tolist(), tot))
     finally:
         dist.destroy_process_group()
