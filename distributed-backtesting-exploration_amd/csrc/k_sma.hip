@@ -130,15 +130,16 @@ __device__ __forceinline__ uint32_t grab_issue(uint32_t* ctr, int lane) {
     return v;
 }
 
-// floor(F / W) for the exact window sum F (< 2^53 as a double): one multiply by an
-// approximate reciprocal, then an exact remainder fix-up.
-__device__ __forceinline__ int32_t floor_key(double F, int W, double iw) {
-    const double fl = floor(F * iw);                       // within 1 of floor(F / W)
-    const double r = F - fl * (double)W;                   // exact
-    int32_t key = (int32_t)fl;
-    key -= (int32_t)(r < 0.0);
-    key += (int32_t)(r >= (double)W);
-    return key;
+// floor(F / W) for the exact window sum F (an integer < 2^53 held as a double, F/W < 2^31,
+// W <= 4096): one multiply by an UPWARD-biased reciprocal iw = RN(RN(1/W) * (1 + 2^-45)) and a
+// truncating conversion, no fix-up. With two roundings of at most 2^-53 relative each, the
+// computed product is F/W * (1 + e) with 2^-46 < e < 2^-44, and its own rounding (2^-53
+// relative) cannot undo the bias, so p >= F/W; and p - F/W <= 2^31 * 2^-44 = 2^-13 < 1/W, while
+// F/W = n + r/W sits at least 1/W below n + 1. Hence trunc(p) == floor(F/W) exactly
+// (tests/test_oracle_golden.py::test_biased_reciprocal_floor checks it exhaustively near every
+// multiple for all W <= 4096).
+__device__ __forceinline__ int32_t floor_key(double F, double iw) {
+    return (int32_t)(F * iw);
 }
 
 __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R, const double* ring,
@@ -175,7 +176,7 @@ __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R,
 #pragma unroll
         for (int q = 0; q < kKeyGrab; ++q) {
             if (w + q < (uint32_t)nw) {
-                const int32_t kq = floor_key(Fv[q], Wv[q], Iv[q]);
+                const int32_t kq = floor_key(Fv[q], Iv[q]);
                 K[(w + q) * kKS + lane] =
                     (tin && t + 1 - Wv[q] >= 0) ? kq : ((int)(w + q) < nf ? -1 : -2);
             }
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
     for (int w = tid; w < nw; w += blockDim.x) {
         const int W = w < nf ? g.a[w] : g.b[w - nf];
         win[w] = W;
-        invw[w] = 1.0 / (double)W;
+        invw[w] = key_recip(W);
     }
     if (tid == 0) {
         ring[0] = 0.0;
