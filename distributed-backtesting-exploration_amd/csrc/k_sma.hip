@@ -196,8 +196,8 @@ __device__ __forceinline__ void cmp4(uint32_t& l, uint32_t& z, const int4& x, co
     l = __builtin_amdgcn_alignbit(l, d1, 31);
     l = __builtin_amdgcn_alignbit(l, d2, 31);
     l = __builtin_amdgcn_alignbit(l, d3, 31);
-    z = min(z, min(d0, d1));
-    z = min(z, min(d2, d3));
+    z = min(min(z, d0), d1);   // one v_min3_u32 per two bars
+    z = min(min(z, d2), d3);
 }
 
 // Equality word for the rare tiles with equal keys (same bit order as cmp4).
@@ -226,56 +226,83 @@ struct SmaAcct {
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
 };
 
+// SMA positions: flat until the first decision, then every flip reverses (fast > slow is
+// long, fast < slow short), and the forced exit at bar B-1 goes flat. So a tile's flips are at
+// most one entry from flat, then reversals (a branch-free loop), then at most the forced exit.
+
+// Closes the open trade at in-tile bar b (fill cx = close of bar t = t0 + b).
 template <bool PARITY>
-__device__ __forceinline__ void sma_flip(SmaAcct& a, int b, int t0, int bl, uint64_t LONG,
-                                         const int32_t* cT, const int64_t* ql, const Agg* D,
-                                         bt_trade* tr, int cap) {
-    const int t = t0 + b;
-    const int32_t cx = cT[b];
-    const uint64_t qx = (uint64_t)ql[b];
-    const int pos = a.pos;
-    // SMA: after the first decision every flip reverses; the forced exit at B-1 goes flat
-    const int np = b == bl ? 0 : (pos != 0 ? -pos : (((LONG >> b) & 1) ? 1 : -1));
-    if (pos != 0) {
-        const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, b));
-        const bool lg = pos > 0;
-        const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
-        const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
-        const int32_t path = lg ? st.dd : st.du;
-        const int32_t pnl = lg ? cx - a.ce : a.ce - cx;
-        a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
-        a.gap = max(a.gap, (int64_t)hi) - pnl;
-        a.R += pnl;
-        a.expo += t - a.e;
-        const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
-                           ((uint64_t)lg << 62);
-        a.h = (a.h ^ w) * kFnvPrime;
-        if (PARITY && a.ntr < cap) {
-            bt_trade r;
-            r.entry_bar = a.e;
-            r.exit_bar = t;
-            r.side = pos;
-            r.pad = 0;
-            r.entry_px = a.ce;
-            r.exit_px = cx;
-            tr[a.ntr] = r;
-        }
-        a.ntr++;
+__device__ __forceinline__ void sma_close(SmaAcct& a, int b, int t, int32_t cx, const Agg* D,
+                                          bt_trade* tr, int cap) {
+    const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, b));
+    const bool lg = a.pos > 0;
+    const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
+    const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
+    const int32_t path = lg ? st.dd : st.du;
+    const int32_t pnl = lg ? cx - a.ce : a.ce - cx;
+    a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+    a.gap = max(a.gap, (int64_t)hi) - pnl;
+    a.R += pnl;
+    a.expo += t - a.e;
+    const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
+                       ((uint64_t)lg << 62);
+    a.h = (a.h ^ w) * kFnvPrime;
+    if (PARITY && a.ntr < cap) {
+        bt_trade r;
+        r.entry_bar = a.e;
+        r.exit_bar = t;
+        r.side = a.pos;
+        r.pad = 0;
+        r.entry_px = a.ce;
+        r.exit_px = cx;
+        tr[a.ntr] = r;
     }
-    // Sharpe partials: a close adds +pos * QL[b], an open subtracts np * QL[b] (a reversal adds
-    // 2 pos QL[b]); the squared sum only changes on the first entry and the forced exit
-    a.ps1 += (uint64_t)((int64_t)(pos - np) * (int64_t)qx);
-    if (pos == 0 || np == 0) {
-        const uint64_t q2x = (uint64_t)ql[kTile + b];
-        a.ps2 += pos == 0 ? (uint64_t)0 - q2x : q2x;
-    }
-    if (np != 0) {
-        a.e = t;
-        a.ce = cx;
-        a.sb = b;
-        a.agg = kAggId;
-    }
+    a.ntr++;
+}
+
+__device__ __forceinline__ void sma_open(SmaAcct& a, int b, int t, int32_t cx, int np) {
+    a.e = t;
+    a.ce = cx;
+    a.sb = b;
+    a.agg = kAggId;
     a.pos = np;
+}
+
+// The tile's flips F (bar order). Sharpe partials: a close adds +pos * QL[b], an open subtracts
+// np * QL[b] (a reversal adds 2 pos QL[b]); the squared sum changes only on the first entry
+// (-Q2L[b]) and the forced exit (+Q2L[b]).
+template <bool PARITY>
+__device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl, uint64_t LONG,
+                                          const int32_t* cT, const int64_t* ql, const Agg* D,
+                                          bt_trade* tr, int cap) {
+    const uint64_t FX = (bl >= 0 && bl < 64) ? (F & (1ULL << bl)) : 0ULL;  // forced exit
+    F ^= FX;
+    if (a.pos == 0 && F != 0) {  // the entry from flat (once per lane)
+        const int b = __builtin_ctzll(F);
+        F &= F - 1;
+        const int np = ((LONG >> b) & 1) ? 1 : -1;
+        const uint64_t qx = (uint64_t)ql[b];
+        a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
+        a.ps2 -= (uint64_t)ql[kTile + b];
+        sma_open(a, b, t0 + b, cT[b], np);
+    }
+    while (F) {  // reversals; a wave iterates max(flips per lane) times
+        const int b = __builtin_ctzll(F);
+        F &= F - 1;
+        const int32_t cx = cT[b];
+        const uint64_t q2 = (uint64_t)ql[b] << 1;
+        sma_close<PARITY>(a, b, t0 + b, cx, D, tr, cap);
+        a.ps1 += a.pos > 0 ? q2 : (uint64_t)0 - q2;
+        sma_open(a, b, t0 + b, cx, -a.pos);
+    }
+    if (FX) {  // flat after bar B-1 (only set when a position is open before it)
+        const int b = bl;
+        const uint64_t qx = (uint64_t)ql[b];
+        sma_close<PARITY>(a, b, t0 + b, cT[b], D, tr, cap);
+        a.ps1 += a.pos > 0 ? qx : (uint64_t)0 - qx;
+        a.ps2 += (uint64_t)ql[kTile + b];
+        a.pos = 0;
+    }
 }
 
 template <bool PARITY, bool STAMPS>
@@ -470,12 +497,7 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
                 asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
                 Fw = 0;
             }
-            // one loop over the 64-bit word: a wave iterates max(flips per lane) times
-            while (Fw) {  // ---- trade events of this tile, in bar order
-                const int b = __builtin_ctzll(Fw);
-                Fw &= Fw - 1;
-                sma_flip<PARITY>(a, b, t0, bl, LONG, cT, ql, D, tr, cap);
-            }
+            sma_flips<PARITY>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
             BT_STAMP(4)
             if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
                 a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
