@@ -442,55 +442,63 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
             BT_STAMP(2)
             uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
             const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
-            uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
             const int wb = warm - t0;
-            vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
-            uint64_t G, T = 0;
-            if (z != 0) {
-                G = ~L & vm;
-            } else {  // some bar has equal floor keys: settle those exactly
-                const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
-                G = ~(L | E) & vm;
-                T = E & vm;
+            const int bl = B - 1 - t0;       // forced exit: flat after bar B-1
+            uint64_t LONG, F;
+            if (z != 0 && wb <= 0 && lastdec >= 63) {
+                // every bar decides and no keys are equal: the position after bar b is simply
+                // long iff fast > slow (LONG = G = ~L), and the flips are its changes
+                LONG = ~L;
+                F = (LONG ^ ((LONG << 1) | (uint64_t)(a.pos == 1))) | (uint64_t)(a.pos == 0);
+            } else {
+                uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
+                vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
+                uint64_t G, T = 0;
+                if (z != 0) {
+                    G = ~L & vm;
+                } else {  // some bar has equal floor keys: settle those exactly
+                    const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
+                    G = ~(L | E) & vm;
+                    T = E & vm;
+                }
+                L &= vm;
+                while (T) {
+                    const int b = __builtin_ctzll(T);
+                    T &= T - 1;
+                    const int t = t0 + b;
+                    const double top = ring[(t + 1) & (R - 1)];
+                    const double Fs = (top - ring[(t + 1 - fw) & (R - 1)]) * (double)sw;
+                    const double Lf = (top - ring[(t + 1 - sw) & (R - 1)]) * (double)fw;
+                    G |= (uint64_t)(Fs > Lf) << b;
+                    L |= (uint64_t)(Fs < Lf) << b;
+                }
+                // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
+                uint64_t SHORT;
+                {
+                    const uint64_t A = ~L;
+                    const uint64_t s1 = A + G;
+                    uint64_t cout = s1 < A;
+                    const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
+                    cout |= sum < s1;
+                    LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
+                }
+                {
+                    const uint64_t A = ~G;
+                    const uint64_t s1 = A + L;
+                    uint64_t cout = s1 < A;
+                    const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
+                    cout |= sum < s1;
+                    SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
+                }
+                if (bl < 64) {
+                    const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
+                    LONG &= keep;
+                    SHORT &= keep;
+                }
+                const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
+                const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
+                F = (LONG ^ pL) | (SHORT ^ pS);
             }
-            L &= vm;
-            while (T) {
-                const int b = __builtin_ctzll(T);
-                T &= T - 1;
-                const int t = t0 + b;
-                const double top = ring[(t + 1) & (R - 1)];
-                const double Fs = (top - ring[(t + 1 - fw) & (R - 1)]) * (double)sw;
-                const double Lf = (top - ring[(t + 1 - sw) & (R - 1)]) * (double)fw;
-                G |= (uint64_t)(Fs > Lf) << b;
-                L |= (uint64_t)(Fs < Lf) << b;
-            }
-            // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
-            uint64_t LONG, SHORT;
-            {
-                const uint64_t A = ~L;
-                const uint64_t s1 = A + G;
-                uint64_t cout = s1 < A;
-                const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
-                cout |= sum < s1;
-                LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
-            }
-            {
-                const uint64_t A = ~G;
-                const uint64_t s1 = A + L;
-                uint64_t cout = s1 < A;
-                const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
-                cout |= sum < s1;
-                SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
-            }
-            const int bl = B - 1 - t0;  // forced exit: flat after bar B-1
-            if (bl < 64) {
-                const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
-                LONG &= keep;
-                SHORT &= keep;
-            }
-            const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
-            const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
-            const uint64_t F = (LONG ^ pL) | (SHORT ^ pS);
             BT_STAMP(3)
             uint64_t Fw = F;
             if (g.ablate & 8) {  // profiling: drop the trade events (keep F live)
