@@ -43,9 +43,10 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
     L.ring = take((size_t)ring * 8);
-    L.keys = take((size_t)2 * nw * kKS * 4);
-    L.invw = take((size_t)(nw + kKeyGrab) * 8);   // + pad: key groups read whole 16-B words
-    L.win = take((size_t)(nw + kKeyGrab) * 4);
+    const int nwp = (nw + kKeyGrab - 1) / kKeyGrab * kKeyGrab;  // key rows: whole groups
+    L.keys = take((size_t)2 * nwp * kKS * 4);
+    L.invw = take((size_t)nwp * 8);
+    L.win = take((size_t)nwp * 4);
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
@@ -142,20 +143,22 @@ __device__ __forceinline__ int32_t floor_key(double F, double iw) {
     return (int32_t)(F * iw);
 }
 
-__device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R, const double* ring,
-                                           const int32_t* win, const double* invw, int32_t* K,
-                                           uint32_t* ctr, uint32_t round, int nwaves, int lane) {
+__device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nwp, int nf, int wmax, int R,
+                                           const double* ring, const int32_t* win,
+                                           const double* invw, int32_t* K, uint32_t* ctr,
+                                           uint32_t round, int nwaves, int lane) {
     const int t = t0 + lane;
     const double top = ring[(t + 1) & (R - 1)];
-    const bool tin = t < B;
-    const uint32_t per = (uint32_t)kKeyGrab * ((uint32_t)(nw + kKeyGrab - 1) / kKeyGrab + nwaves);
+    // wave-uniform: every bar of the tile has a full window for every window length
+    const bool full = t0 + 1 - wmax >= 0 && t0 + kTile <= B;
+    const uint32_t per = (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + nwaves);
     const uint32_t base = round * per;
     uint32_t w = __builtin_amdgcn_readlane(grab_issue(ctr, lane), 0) - base;
 #pragma unroll 1
-    while (w < (uint32_t)nw) {
+    while (w < (uint32_t)nwp) {
         const uint32_t vn = grab_issue(ctr, lane);  // next group, read at the end
         // w is a multiple of kKeyGrab: the group's lengths and reciprocals are aligned 16-B
-        // reads (the LDS regions are padded; entries past nw are never used)
+        // reads; rows nw..nwp-1 are padding (length 1) whose keys nobody reads
         int Wv[kKeyGrab];
         double Iv[kKeyGrab], Fv[kKeyGrab];
 #pragma unroll
@@ -170,15 +173,19 @@ __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nf, int R,
         }
 #pragma unroll
         for (int q = 0; q < kKeyGrab; ++q) {
-            Wv[q] = __builtin_amdgcn_readfirstlane(w + q < (uint32_t)nw ? Wv[q] : Wv[0]);
+            Wv[q] = __builtin_amdgcn_readfirstlane(Wv[q]);
             Fv[q] = top - ring[(t + 1 - Wv[q]) & (R - 1)];  // exact (< 2^53)
         }
+        int32_t* Kw = K + w * kKS + lane;
+        if (full) {
 #pragma unroll
-        for (int q = 0; q < kKeyGrab; ++q) {
-            if (w + q < (uint32_t)nw) {
+            for (int q = 0; q < kKeyGrab; ++q) Kw[q * kKS] = floor_key(Fv[q], Iv[q]);
+        } else {
+            const bool tin = t < B;
+#pragma unroll
+            for (int q = 0; q < kKeyGrab; ++q) {
                 const int32_t kq = floor_key(Fv[q], Iv[q]);
-                K[(w + q) * kKS + lane] =
-                    (tin && t + 1 - Wv[q] >= 0) ? kq : ((int)(w + q) < nf ? -1 : -2);
+                Kw[q * kKS] = (tin && t + 1 - Wv[q] >= 0) ? kq : ((int)(w + q) < nf ? -1 : -2);
             }
         }
         w = __builtin_amdgcn_readlane(vn, 0) - base;
@@ -306,7 +313,7 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
 }
 
 template <bool PARITY, bool STAMPS>
-__global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ syms,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(const SymDesc* __restrict__ syms,
                                                    const int32_t* __restrict__ close, Grid g,
                                                    Out out, int dedicated) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -349,8 +356,9 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
     const int p = (kf * ns) + (ks - nf);
     const int32_t* crow = close + sd.off;
 
-    for (int w = tid; w < nw; w += blockDim.x) {
-        const int W = w < nf ? g.a[w] : g.b[w - nf];
+    const int nwp = (nw + kKeyGrab - 1) / kKeyGrab * kKeyGrab;
+    for (int w = tid; w < nwp; w += blockDim.x) {
+        const int W = w < nf ? g.a[w] : (w < nw ? g.b[w - nf] : 1);
         win[w] = W;
         invw[w] = key_recip(W);
     }
@@ -379,7 +387,7 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
     } else {
         __syncthreads();
     }
-    stage_keys(0, B, nw, nf, R, ring, win, invw, keys, ctr, 0, nwaves, lane);
+    stage_keys(0, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys, ctr, 0, nwaves, lane);
     __syncthreads();
 
     SmaAcct a;
@@ -425,7 +433,7 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
             const Agg* D = dst + s * kDstLevels * kTile;
-            const int32_t* K = keys + (k & 1) * nw * kKS;
+            const int32_t* K = keys + (k & 1) * nwp * kKS;
             const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
             const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
             uint32_t l0 = 0, l1 = 0, z = ~0u;
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(1024) void sma_kernel(const SymDesc* __restrict__ s
             BT_STAMP(5)
         }
         if (k + 1 < ntiles && !(g.ablate & 2))
-            stage_keys(t0 + kTile, B, nw, nf, R, ring, win, invw, keys + ((k + 1) & 1) * nw * kKS,
+            stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
                        ctr, (uint32_t)(k + 1), nwaves, lane);
         BT_STAMP(1)
         __syncthreads();
