@@ -51,8 +51,8 @@ __device__ __forceinline__ Agg dst_query_bf(const Agg* D, int a, int b) {
     return agg_merge(D[L * kTile + a], D[L * kTile + b]);
 }
 
-// Upward-biased reciprocal for exact floor keys (k_sma.hip floor_key): RN(RN(1/W) * (1 + 2^-45)).
-__host__ __device__ inline double key_recip(int W) { return (1.0 / (double)W) * (1.0 + 0x1p-45); }
+// Upward-biased reciprocal for exact floor keys (k_sma.hip floor_key): RN(RN(1/W) * (1 + 2^-47)).
+__host__ __device__ inline double key_recip(int W) { return (1.0 / (double)W) * (1.0 + 0x1p-47); }
 
 // Identity of agg_merge: merge(kAggId, x) == x for prices in [1, 2^31) (no int32 overflow:
 // 0 - x.mn < 0 and x.mx - INT32_MAX <= 0).

@@ -131,14 +131,14 @@ __device__ __forceinline__ uint32_t grab_issue(uint32_t* ctr, int lane) {
     return v;
 }
 
-// floor(F / W) for the exact window sum F (an integer < 2^53 held as a double, F/W < 2^31,
-// W <= 4096): one multiply by an UPWARD-biased reciprocal iw = RN(RN(1/W) * (1 + 2^-45)) and a
-// truncating conversion, no fix-up. With two roundings of at most 2^-53 relative each, the
-// computed product is F/W * (1 + e) with 2^-46 < e < 2^-44, and its own rounding (2^-53
-// relative) cannot undo the bias, so p >= F/W; and p - F/W <= 2^31 * 2^-44 = 2^-13 < 1/W, while
-// F/W = n + r/W sits at least 1/W below n + 1. Hence trunc(p) == floor(F/W) exactly
-// (tests/test_oracle_golden.py::test_biased_reciprocal_floor checks it exhaustively near every
-// multiple for all W <= 4096).
+// floor(F / W) for the exact window sum F (an integer < 2^53 held as a double, F/W < 2^31):
+// one multiply by an UPWARD-biased reciprocal iw = RN(RN(1/W) * (1 + 2^-47)) and a truncating
+// conversion, no fix-up. Three roundings of at most 2^-53 relative each leave the computed
+// product p = F/W * (1 + e) with 2^-47 * (1 - 3/64) < e < 2^-47 * (1 + 3/64): the bias is never
+// undone, so p >= F/W, and p - F/W < 2^31 * 2^-46.9 = 2^-15.9 < 1/W for every W < 62,000
+// (the LDS ring caps SMA windows near 16,000), while F/W = n + r/W sits at least 1/W below
+// n + 1. Hence trunc(p) == floor(F/W) exactly (tests/test_oracle_golden.py::
+// test_biased_reciprocal_floor checks all W <= 16,384 at and around multiples of W).
 __device__ __forceinline__ int32_t floor_key(double F, double iw) {
     return (int32_t)(F * iw);
 }
@@ -585,7 +585,8 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     if (n_sym <= 0) return hipSuccess;
     const SmaShape sh = sma_shape(g.n_params);
     const dim3 grid(n_sym, sh.gy), block(sh.block);
-    const size_t lds = sma_lds_bytes(g);
+    size_t lds = sma_lds_bytes(g);
+    if (g.ablate & 128) lds = std::max(lds, (size_t)(g.ablate & 256 ? 80 : 60) * 1024);  // occupancy probe
     if (g.ablate & 64)
         hipLaunchKernelGGL((sma_kernel<false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity)

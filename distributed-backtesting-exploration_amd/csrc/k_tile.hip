@@ -638,6 +638,12 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 // parameter wave per symbol on config 3 and is latency-bound at ~1.5 waves per SIMD: two extra
 // waves take 4.96 -> 3.68 ms. The Bollinger kernel already runs 5 waves x 2 blocks per CU and
 // its 122 VGPRs cap a CU at 16 waves: extra waves only cost it (12.4 -> 12.9 ms with 2).
+static int tile_param_waves(int need, int cap) {
+    int pw = std::min(need, cap);
+    if (const char* v = getenv("BT_PW")) pw = std::max(1, std::min(atoi(v), pw));  // tuning aid
+    return pw;
+}
+
 static int tile_extra_waves(int used, int x) {
     if (const char* v = getenv("BT_XW")) x = atoi(v);  // tuning aid
     return std::max(0, std::min(x, 16 - used));
@@ -649,7 +655,7 @@ size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = std::min((g.n_params + 63) / 64, 1024 / 64 - 2);
+    const int pw = tile_param_waves((g.n_params + 63) / 64, 1024 / 64 - 2);
     const int xw = tile_extra_waves(pw + 2, 2);
     const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
     const dim3 block(64 * (pw + 2 + xw));
@@ -667,7 +673,7 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
                        hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = std::min((g.n_params + 63) / 64, 1024 / 64 - 1);
+    const int pw = tile_param_waves((g.n_params + 63) / 64, 1024 / 64 - 1);
     const int xw = tile_extra_waves(pw + 1, 0);
     const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
     const dim3 block(64 * (pw + 1 + xw));

@@ -125,13 +125,14 @@ def test_numpy_restatement_matches_c_fresh():
 
 def test_biased_reciprocal_floor():
     """k_sma.hip floor_key: trunc(F * key_recip(W)) == floor(F / W) for every window length the
-    spec allows (W <= 4096) and F/W < 2^31, checked at and around every tested multiple of W
-    (the only places a rounding error could move the truncation)."""
+    SMA kernel can hold (W <= 16,384; its LDS ring caps windows near 16,000) and F/W < 2^31,
+    checked at and around every tested multiple of W (the only places a rounding error could
+    move the truncation)."""
     rng = np.random.default_rng(11)
-    W = np.arange(1, 4097, dtype=np.int64)[:, None]
-    iw = (1.0 / W.astype(np.float64)) * (1.0 + 2.0 ** -45)   # device_common.h key_recip
+    W = np.arange(1, 16385, dtype=np.int64)[:, None]
+    iw = (1.0 / W.astype(np.float64)) * (1.0 + 2.0 ** -47)   # device_common.h key_recip
     n = np.concatenate([[0, 1, 2, 10_000, 2 ** 31 - 2, 2 ** 31 - 1],
-                        rng.integers(1, 2 ** 31 - 1, 250)]).astype(np.int64)[None, :]
+                        rng.integers(1, 2 ** 31 - 1, 120)]).astype(np.int64)[None, :]
     for r in (lambda w: 0 * w, lambda w: np.minimum(1, w - 1), lambda w: w - 1, lambda w: w // 2,
               lambda w: rng.integers(0, 1 << 20, w.shape) % w):
         rem = r(W)
