@@ -437,15 +437,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
             const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
             uint32_t l0 = 0, l1 = 0, z = ~0u;
-#pragma unroll 1
-            for (int v0 = 0; v0 < 8 && !(g.ablate & 4); v0 += 2) {
+            if (!(g.ablate & 4)) {
+                // all reads at immediate offsets from one address per row
 #pragma unroll
-                for (int v = v0; v < v0 + 2; ++v) cmp4(l0, z, k1[v], k2[v]);
-            }
-#pragma unroll 1
-            for (int v0 = 8; v0 < 16 && !(g.ablate & 4); v0 += 2) {
-#pragma unroll
-                for (int v = v0; v < v0 + 2; ++v) cmp4(l1, z, k1[v], k2[v]);
+                for (int v = 0; v < 16; ++v) {
+                    if (v < 8) cmp4(l0, z, k1[v], k2[v]);
+                    else cmp4(l1, z, k1[v], k2[v]);
+                    // keep the schedule to two int4 pairs in flight (VGPR budget)
+                    if (v & 1) __builtin_amdgcn_sched_barrier(0);
+                }
             }
             BT_STAMP(2)
             uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
