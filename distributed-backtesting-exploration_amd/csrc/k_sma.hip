@@ -226,7 +226,8 @@ __device__ __forceinline__ uint64_t eq_word(const int32_t* k1, const int32_t* k2
 //    the tile end: entry at bar b adds -side*QL[b], exit adds +side*QL[b], an open position
 //    at the tile end adds +side*QL[63].
 struct SmaAcct {
-    int32_t pos, e, ce, sb, ntr, expo;   // sb: in-tile bar where the open trade's path resumes
+    int32_t pos, e, ce, sb, ntr, e0;     // sb: in-tile bar where the open trade's path resumes;
+                                         // e0: first entry bar
     int64_t R, gap, mdd;
     uint64_t ps1, ps2, h;
     i128 s1, s2;
@@ -250,7 +251,6 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, int b, int t, int32_t cx, 
     a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
     a.gap = max(a.gap, (int64_t)hi) - pnl;
     a.R += pnl;
-    a.expo += t - a.e;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)lg << 62);
     a.h = (a.h ^ w) * kFnvPrime;
@@ -291,6 +291,7 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
         const uint64_t qx = (uint64_t)ql[b];
         a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
         a.ps2 -= (uint64_t)ql[kTile + b];
+        a.e0 = t0 + b;
         sma_open(a, b, t0 + b, cT[b], np);
     }
     while (F) {  // reversals; a wave iterates max(flips per lane) times
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     __syncthreads();
 
     SmaAcct a;
-    a.pos = a.e = a.ce = a.sb = a.ntr = a.expo = 0;
+    a.pos = a.e = a.ce = a.sb = a.ntr = a.e0 = 0;
     a.R = a.gap = a.mdd = 0;
     a.ps1 = a.ps2 = 0;
     a.h = kFnvOff;
@@ -549,7 +550,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         r.status = 0;
         r.pnl = a.R;
         r.mdd = a.mdd;
-        r.exposure = a.expo;
+        // bars held: trades are back to back from the first entry to the forced exit at B-1
+        r.exposure = a.ntr > 0 ? B - 1 - a.e0 : 0;
         r.sharpe = sh;
         r.hash = a.h;
         out.sum[gi] = r;
