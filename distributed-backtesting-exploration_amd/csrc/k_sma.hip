@@ -294,15 +294,19 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
         a.e0 = t0 + b;
         sma_open(a, b, t0 + b, cT[b], np);
     }
-    while (F) {  // reversals; a wave iterates max(flips per lane) times
+    // reversals; a wave iterates max(flips per lane) times. The k-th reversal closes side
+    // p_k = (-1)^(k-1) p_1 and adds 2 p_k QL[b_k]: an alternating sum, carried as
+    // alt_k = QL[b_k] - alt_(k-1), so that sum = 2 p_n alt_n = -2 pos alt after the loop
+    uint64_t alt = 0;
+    while (F) {
         const int b = __builtin_ctzll(F);
         F &= F - 1;
         const int32_t cx = cT[b];
-        const uint64_t q2 = (uint64_t)ql[b] << 1;
+        alt = (uint64_t)ql[b] - alt;
         sma_close<PARITY>(a, b, t0 + b, cx, D, tr, cap);
-        a.ps1 += a.pos > 0 ? q2 : (uint64_t)0 - q2;
         sma_open(a, b, t0 + b, cx, -a.pos);
     }
+    a.ps1 += a.pos > 0 ? (uint64_t)0 - (alt << 1) : alt << 1;
     if (FX) {  // flat after bar B-1 (only set when a position is open before it)
         const int b = bl;
         const uint64_t qx = (uint64_t)ql[b];
