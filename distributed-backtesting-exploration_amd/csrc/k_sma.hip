@@ -240,9 +240,9 @@ struct SmaAcct {
 
 // Closes the open trade at in-tile bar b (fill cx = close of bar t = t0 + b).
 template <bool PARITY>
-__device__ __forceinline__ void sma_close(SmaAcct& a, int b, int t, int32_t cx, const Agg* D,
+__device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int32_t cx,
                                           bt_trade* tr, int cap) {
-    const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, b));
+    const Agg st = agg_merge(a.agg, seg);   // seg: closes [sb, b] of this tile
     const bool lg = a.pos > 0;
     const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
     const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
@@ -301,16 +301,17 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     while (F) {
         const int b = __builtin_ctzll(F);
         F &= F - 1;
+        const Agg seg = dst_query_bf(D, a.sb, b);  // issued first: addresses need only b
         const int32_t cx = cT[b];
         alt = (uint64_t)ql[b] - alt;
-        sma_close<PARITY>(a, b, t0 + b, cx, D, tr, cap);
+        sma_close<PARITY>(a, seg, t0 + b, cx, tr, cap);
         sma_open(a, b, t0 + b, cx, -a.pos);
     }
     a.ps1 += a.pos > 0 ? (uint64_t)0 - (alt << 1) : alt << 1;
     if (FX) {  // flat after bar B-1 (only set when a position is open before it)
         const int b = bl;
         const uint64_t qx = (uint64_t)ql[b];
-        sma_close<PARITY>(a, b, t0 + b, cT[b], D, tr, cap);
+        sma_close<PARITY>(a, dst_query_bf(D, a.sb, b), t0 + b, cT[b], tr, cap);
         a.ps1 += a.pos > 0 ? qx : (uint64_t)0 - qx;
         a.ps2 += (uint64_t)ql[kTile + b];
         a.pos = 0;
