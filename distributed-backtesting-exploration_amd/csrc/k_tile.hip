@@ -166,6 +166,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     auto chain = [&](int T, int32_t cl) {
         const int t1 = T * kTile;
         double* E = ebuf + (T & 1) * estage + lane * kEStride;
+        // the chain is the block's per-tile critical path (three dependent fp64 operations per
+        // bar): issue it ahead of the other waves on its SIMD
+        if (!(g.ablate & 32)) __builtin_amdgcn_s_setprio(3);
         if (lane < nsp) {
             if (t1 > 0 && t1 + kTile <= B) {
 #pragma unroll
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 }
             }
         }
+        __builtin_amdgcn_s_setprio(0);
     };
 
     // condition words of tile T, tasks grabbed dynamically (round T), lane = bar
