@@ -1,0 +1,84 @@
+"""Randomised GPU parity sweep: seeded random grids, ragged series lengths and tie-prone price
+paths for all three strategies, every result field and every trade bit-exact vs the C oracle.
+
+The price paths are chosen to reach the kernels' rare branches: narrow integer walks (equal SMA
+floor keys, exact SMA ties, flat stretches), plateaus, spikes near the 2^31-tick ceiling, and
+lengths that end mid-tile, exactly on a tile edge or before the longest window fills.
+"""
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from helpers import compare_summary, compare_trades, oracle_row
+
+pytestmark = pytest.mark.gpu
+
+CAP = 4096
+
+
+def _series(rng, n, kind):
+    if kind == "walk":          # ordinary tick walk around $100
+        x = 1_000_000 + np.cumsum(rng.integers(-4000, 4001, n))
+    elif kind == "narrow":      # a few ticks wide: floor keys and exact SMAs collide often
+        x = 10_000 + np.cumsum(rng.integers(-1, 2, n))
+        x = np.clip(x, 10_000, 10_004)
+    elif kind == "plateau":     # long flat stretches with rare jumps
+        x = 20_000 + 50 * np.cumsum(rng.random(n) < 0.03)
+    else:                       # "spiky": near the int32 price ceiling with large moves
+        x = 2_000_000_000 + np.cumsum(rng.integers(-3_000_000, 3_000_001, n))
+    return np.clip(x, 10_000, 2**31 - 1).astype(np.int32)
+
+
+def _ohlc(rng, c):
+    hi = c + rng.integers(0, 3000, len(c)).astype(np.int64)
+    lo = c - rng.integers(0, 3000, len(c)).astype(np.int64)
+    return np.clip(hi, 1, 2**31 - 1).astype(np.int32), np.clip(lo, 1, 2**31 - 1).astype(np.int32)
+
+
+def _windows(rng, k, top):
+    return sorted(set(int(x) for x in rng.integers(1, top, k)))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_sma(seed):
+    rng = np.random.default_rng(1000 + seed)
+    grid = D.Grid.sma(_windows(rng, 7, 40), _windows(rng, 6, 300), annualization=252)
+    kinds = ["walk", "narrow", "plateau", "spiky"]
+    closes = [_series(rng, int(n), kinds[i % 4])
+              for i, n in enumerate(rng.choice([1, 2, 63, 64, 65, 127, 128, 300, 777, 1500], 8))]
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_ohlc(closes)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("sma", grid, (cl, cl, cl, cl), 252, CAP)
+        for p in range(grid.n_params):
+            where = f"seed {seed} sym {s} len {len(cl)} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("ema_ols", "boll") for s in range(5)])
+def test_random_tile_strategies(strategy, seed):
+    rng = np.random.default_rng(2000 + seed + (100 if strategy == "boll" else 0))
+    if strategy == "ema_ols":
+        grid = D.Grid.ema_ols(_windows(rng, 4, 200), _windows(rng, 4, 400),
+                              band_bps=int(rng.integers(0, 60)))
+    else:
+        grid = D.Grid.boll(_windows(rng, 3, 120), sorted(set(int(x) for x in rng.integers(1, 7, 3))),
+                           [int(x) for x in rng.integers(10, 300, 2)],
+                           [int(x) for x in rng.integers(10, 500, 2)], k_den=2)
+    kinds = ["walk", "narrow", "plateau", "spiky"]
+    closes = [_series(rng, int(n), kinds[i % 4])
+              for i, n in enumerate(rng.choice([1, 2, 64, 65, 129, 500, 2000], 6))]
+    highs, lows = zip(*[_ohlc(rng, c) for c in closes])
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_ohlc(closes, list(highs), list(lows))
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row(strategy, grid, (cl, highs[s], lows[s], cl), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} seed {seed} sym {s} len {len(cl)} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
