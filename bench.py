@@ -3,10 +3,12 @@
 Default workload (N=1 and per GPU for N>1): BASELINE config 2 — SMA fast/slow crossover,
 5,000 symbols x 2,520 daily bars x 400 param pairs, synthetic OHLC (docs/oracle_spec.md §1)
 generated directly in HBM before timing. One step = one pass of the hot path over that batch:
-the fused strategy kernel (indicators + signals + position/PnL/drawdown/Sharpe per lane) and the
-per-GPU top-k; for N>1 also the RCCL all-gather of the top-k records + all-reduce of counters
-(the only exchange step). Symbols are sharded across ranks with no data-path
-collective (weak scaling: every rank runs its own shard).
+the fused strategy kernel (indicators + signals + position/PnL/drawdown/Sharpe per lane), the
+per-GPU top-k and its read-back; for N>1 also one RCCL all-gather of every rank's top-k records
+and counters (the only exchange step). Step i+1 is enqueued before step i's
+read-back/exchange is consumed, so host work and the collective overlap the next pass. Symbols
+are sharded across ranks with no data-path collective (weak scaling: every rank runs its own
+shard).
 
 `--config 3|4|5` measures the per-GPU shard of the other BASELINE configs the same way (EMA+OLS
 500 x 98,280 x 64; Bollinger 500 x 98,280 x 256, i.e. 2,000 symbols over 4 GPUs; SMA
@@ -148,18 +150,32 @@ def main():
     eng = D.Engine(grid, device=device, topk=TOPK, timing=True)
     eng.load_synthetic(SEED, rank * S_PER_GPU, S_PER_GPU, BARS, cfg["freq"])
 
-    def step():
-        eng.run()
-        top = eng.read_topk()          # syncs the engine stream
+    def issue(i):
+        eng.run()                      # kernels of step i, enqueued on the engine stream
+        eng.topk_fetch_async(i & 1)    # its top-k + trade count into pinned slot i % 2
+
+    def finish(i):
+        top, trades = eng.topk_fetch_wait(i & 1)
         if dist is None:
             return top
         # the one exchange step: a single RCCL all-gather carrying each rank's k x 24 B top-k
         # records and its run counters (summed on the host)
-        top, _ = PAR.exchange(top, TOPK, [S_PER_GPU * BARS * P, eng.stats()["trades"]], dist)
+        top, _ = PAR.exchange(top, TOPK, [S_PER_GPU * BARS * P, trades], dist)
         return top
 
-    for _ in range(args.warmup):
-        step()
+    def steps(n):
+        """n steps; step i+1 is enqueued before step i's read-back and exchange, so the GPU runs
+        the next pass while the host consumes (and, for N > 1, exchanges) this one."""
+        top = None
+        if n > 0:
+            issue(0)
+        for i in range(n):
+            if i + 1 < n:
+                issue(i + 1)
+            top = finish(i)
+        return top
+
+    steps(args.warmup)
     eng.sync()
     eng.reset_timing()
     if dist is not None:
@@ -167,8 +183,7 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        top = step()
+    top = steps(args.steps)
     eng.sync()
     if dist is not None:
         torch.cuda.synchronize()

@@ -81,17 +81,30 @@ struct bt_engine {
     int64_t rows = 0;
     DevBuf<SymDesc> d_syms;
     DevBuf<int32_t> d_c, d_h, d_l;
-    // outputs
-    DevBuf<bt_summary> d_sum;
-    DevBuf<uint64_t> d_key;
+    // outputs, double-buffered: run i writes buffer i % 2 while the top-k chain of run i-1
+    // (on tstream) still reads the other one; `cur` is the buffer of the last run
+    DevBuf<bt_summary> d_sum[2];
+    DevBuf<uint64_t> d_key[2];
+    DevBuf<unsigned long long> d_ntr[2];
+    int cur = 0;
+    int64_t nrun = 0;
     DevBuf<bt_sums> d_sums;
     DevBuf<bt_trade> d_trades;
-    DevBuf<unsigned long long> d_ntr, d_dbg;
+    DevBuf<unsigned long long> d_dbg;
+    // top-k chain stream: the chain of run i overlaps the kernel of run i+1
+    hipStream_t tstream = nullptr;
+    hipEvent_t ev_kdone = nullptr;          // kernel of the last run finished (main stream)
+    hipEvent_t ev_tdone[2] = {nullptr, nullptr};  // readers of buffer b finished (tstream)
+    bool tdone_armed[2] = {false, false};
     // top-k work
     DevBuf<unsigned int> d_hist, d_counts;
     DevBuf<unsigned long long> d_state, d_above, d_cand;
     DevBuf<bt_topk_rec> d_top;
     bt_topk_rec* h_top = nullptr;     // pinned host copy of d_top
+    // pipelined read-back slots: header + kTopkMax records + one record holding the trade count
+    bt_topk_rec* h_slot[2] = {nullptr, nullptr};
+    hipEvent_t slot_ev[2] = {nullptr, nullptr};
+    bool slot_armed[2] = {false, false};
     bool topk_ready = false;          // top-k buffers allocated and their state initialised
     bool ran = false;
     // timing of the dominant kernel
@@ -234,11 +247,18 @@ TopkWork topk_work(bt_engine* e) {
                     kTopkCap, e->d_top.p + 1, reinterpret_cast<int32_t*>(e->d_top.p)};
 }
 
+void sync_all(bt_engine* e) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (e->tstream) HIPCHK(hipStreamSynchronize(e->tstream));
+}
+
 void ensure_outputs(bt_engine* e) {
     const size_t n = (size_t)e->syms.size() * e->P;
-    e->d_sum.ensure(std::max<size_t>(1, n));
-    e->d_key.ensure(std::max<size_t>(1, n));
-    e->d_ntr.ensure(1);
+    for (int b = 0; b < 2; ++b) {
+        e->d_sum[b].ensure(std::max<size_t>(1, n));
+        e->d_key[b].ensure(std::max<size_t>(1, n));
+        e->d_ntr[b].ensure(1);
+    }
     if (e->cfg.flags & BT_FLAG_PARITY) {
         e->d_sums.ensure(std::max<size_t>(1, n));
         e->d_trades.ensure(std::max<size_t>(1, n * (size_t)e->cfg.trade_cap));
@@ -260,15 +280,19 @@ void run_impl(bt_engine* e) {
     activate(e);
     ensure_outputs(e);
     const int32_t S = (int32_t)e->syms.size();
+    const int b = (int)(e->nrun++ & 1);
+    e->cur = b;
+    // buffer b was last read by the top-k chain / read-back of run i-2: wait for them
+    if (e->tdone_armed[b]) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_tdone[b], 0));
     Out out{};
-    out.sum = e->d_sum.p;
-    out.key = e->d_key.p;
+    out.sum = e->d_sum[b].p;
+    out.key = e->d_key[b].p;
     const bool parity = (e->cfg.flags & BT_FLAG_PARITY) != 0;
     out.sums = parity ? e->d_sums.p : nullptr;
     out.trades = parity ? e->d_trades.p : nullptr;
     out.trade_cap = parity ? e->cfg.trade_cap : 0;
-    out.n_trades = e->d_ntr.p;
-    HIPCHK(hipMemsetAsync(e->d_ntr.p, 0, sizeof(unsigned long long), e->stream));
+    out.n_trades = e->d_ntr[b].p;
+    HIPCHK(hipMemsetAsync(e->d_ntr[b].p, 0, sizeof(unsigned long long), e->stream));
     out.dbg = nullptr;
     if (e->grid.ablate & 64) {  // profiling stamps
         e->d_dbg.ensure(32);
@@ -306,8 +330,12 @@ void run_impl(bt_engine* e) {
         e->ev_pending.push_back(ev);
     }
     if (e->cfg.topk > 0) {
-        HIPCHK(launch_topk(e->d_key.p, e->d_sum.p, e->d_syms.p, (int64_t)S * e->P, e->P,
-                           e->cfg.topk, topk_work(e), e->stream));
+        HIPCHK(hipEventRecord(e->ev_kdone, e->stream));
+        HIPCHK(hipStreamWaitEvent(e->tstream, e->ev_kdone, 0));
+        HIPCHK(launch_topk(e->d_key[b].p, e->d_sum[b].p, e->d_syms.p, (int64_t)S * e->P, e->P,
+                           e->cfg.topk, topk_work(e), e->tstream));
+        HIPCHK(hipEventRecord(e->ev_tdone[b], e->tstream));
+        e->tdone_armed[b] = true;
     }
     e->ran = true;
 }
@@ -336,8 +364,8 @@ std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     // header + the configured k records in one copy into pinned memory
     const size_t nrec = (size_t)e->cfg.topk + 1;
     HIPCHK(hipMemcpyAsync(e->h_top, e->d_top.p, nrec * sizeof(bt_topk_rec), hipMemcpyDeviceToHost,
-                          e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+                          e->tstream));
+    sync_all(e);
     int32_t n = 0;
     memcpy(&n, e->h_top, sizeof n);
     std::vector<bt_topk_rec> res;
@@ -346,7 +374,7 @@ std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     } else {  // more than kTopkCap records tie on the selected prefix: finish on the host
         const size_t total = e->syms.size() * (size_t)e->P;
         std::vector<bt_summary> all(total);
-        HIPCHK(hipMemcpy(all.data(), e->d_sum.p, total * sizeof(bt_summary), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(all.data(), e->d_sum[e->cur].p, total * sizeof(bt_summary), hipMemcpyDeviceToHost));
         res.reserve(total);
         for (size_t i = 0; i < total; ++i) {
             const int32_t s = (int32_t)(i / e->P), p = (int32_t)(i % e->P);
@@ -451,6 +479,9 @@ bt_engine* bt_engine_create(const bt_config* cfg, char* err, size_t errlen) {
             HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
             e->own_stream = true;
         }
+        HIPCHK(hipStreamCreateWithFlags(&e->tstream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e->ev_kdone, hipEventDisableTiming));
+        for (int b = 0; b < 2; ++b) HIPCHK(hipEventCreateWithFlags(&e->ev_tdone[b], hipEventDisableTiming));
         upload_grid(e);
         if (const char* ab = getenv("BT_ABLATE")) e->grid.ablate = atoi(ab);  // profiling aid
         return e;
@@ -468,6 +499,7 @@ void bt_engine_destroy(bt_engine* e) {
     try {
         (void)hipSetDevice(e->cfg.device);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
+        if (e->tstream) (void)hipStreamSynchronize(e->tstream);
         for (auto& ev : e->ev_pending) {
             (void)hipEventDestroy(ev.first);
             (void)hipEventDestroy(ev.second);
@@ -481,11 +513,18 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_c.release();
         e->d_h.release();
         e->d_l.release();
-        e->d_sum.release();
-        e->d_key.release();
+        for (int b = 0; b < 2; ++b) {
+            e->d_sum[b].release();
+            e->d_key[b].release();
+            e->d_ntr[b].release();
+            if (e->ev_tdone[b]) (void)hipEventDestroy(e->ev_tdone[b]);
+            e->ev_tdone[b] = nullptr;
+            e->tdone_armed[b] = false;
+        }
+        if (e->ev_kdone) (void)hipEventDestroy(e->ev_kdone);
+        e->ev_kdone = nullptr;
         e->d_sums.release();
         e->d_trades.release();
-        e->d_ntr.release();
         e->d_dbg.release();
         e->d_hist.release();
         e->d_counts.release();
@@ -495,8 +534,17 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_top.release();
         if (e->h_top) (void)hipHostFree(e->h_top);
         e->h_top = nullptr;
+        for (int i = 0; i < 2; ++i) {
+            if (e->h_slot[i]) (void)hipHostFree(e->h_slot[i]);
+            if (e->slot_ev[i]) (void)hipEventDestroy(e->slot_ev[i]);
+            e->h_slot[i] = nullptr;
+            e->slot_ev[i] = nullptr;
+            e->slot_armed[i] = false;
+        }
         e->topk_ready = false;
         if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+        if (e->tstream) (void)hipStreamDestroy(e->tstream);
+        e->tstream = nullptr;
     } catch (...) {
     }
     delete e;
@@ -518,7 +566,7 @@ int32_t bt_load_synthetic(bt_engine* e, uint64_t seed, int64_t sym_begin, int32_
         layout(e, n_sym, bars.data(), ids.data());
         HIPCHK(launch_gen(e->d_syms.p, n_sym, seed, freq, nullptr, has_hl(e) ? e->d_h.p : nullptr,
                           has_hl(e) ? e->d_l.p : nullptr, e->d_c.p, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         return 0;
     })
 }
@@ -540,7 +588,7 @@ int32_t bt_load_ohlc(bt_engine* e, int32_t n_sym, const int64_t* sym_ids, const 
                 memcpy(tmp.data() + e->syms[s].off, src + row_off[s], (size_t)bars[s] * 4);
             HIPCHK(hipMemcpyAsync(dst, tmp.data(), (size_t)e->rows * 4, hipMemcpyHostToDevice,
                                   e->stream));
-            HIPCHK(hipStreamSynchronize(e->stream));
+            sync_all(e);
         };
         if (e->rows > 0) {
             put(c, e->d_c.p);
@@ -565,7 +613,7 @@ int32_t bt_sync(bt_engine* e) {
     ABI_GUARD(-1, {
         if (!e) throw HipFail{"null engine"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         return 0;
     })
 }
@@ -576,8 +624,8 @@ int32_t bt_read_summaries(bt_engine* e, bt_summary* out, size_t n) {
         const size_t have = e->syms.size() * (size_t)e->P;
         if (n > have) throw HipFail{"n exceeds symbols x params"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
-        HIPCHK(hipMemcpy(out, e->d_sum.p, n * sizeof(bt_summary), hipMemcpyDeviceToHost));
+        sync_all(e);
+        HIPCHK(hipMemcpy(out, e->d_sum[e->cur].p, n * sizeof(bt_summary), hipMemcpyDeviceToHost));
         return 0;
     })
 }
@@ -587,7 +635,7 @@ int32_t bt_read_sums(bt_engine* e, bt_sums* out, size_t n) {
         if (!e || !e->ran || !(e->cfg.flags & BT_FLAG_PARITY)) throw HipFail{"no parity results"};
         if (n > e->syms.size() * (size_t)e->P) throw HipFail{"n too large"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_sums.p, n * sizeof(bt_sums), hipMemcpyDeviceToHost));
         return 0;
     })
@@ -598,7 +646,7 @@ int32_t bt_read_trades(bt_engine* e, bt_trade* out, size_t n) {
         if (!e || !e->ran || !(e->cfg.flags & BT_FLAG_PARITY)) throw HipFail{"no parity results"};
         if (n > e->syms.size() * (size_t)e->P * e->cfg.trade_cap) throw HipFail{"n too large"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_trades.p, n * sizeof(bt_trade), hipMemcpyDeviceToHost));
         return 0;
     })
@@ -614,18 +662,64 @@ int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k) {
     })
 }
 
+int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot) {
+    ABI_GUARD(-1, {
+        if (!e || slot < 0 || slot > 1) throw HipFail{"bad arguments"};
+        if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
+        activate(e);
+        if (!e->h_slot[slot])
+            HIPCHK(hipHostMalloc(&e->h_slot[slot], (kTopkMax + 2) * sizeof(bt_topk_rec)));
+        if (!e->slot_ev[slot]) HIPCHK(hipEventCreateWithFlags(&e->slot_ev[slot], hipEventDisableTiming));
+        bt_topk_rec* h = e->h_slot[slot];
+        // behind the run's top-k chain on tstream; the trade counter of the run's buffer is
+        // complete too (the chain waited for the kernel)
+        HIPCHK(hipMemcpyAsync(h, e->d_top.p, ((size_t)e->cfg.topk + 1) * sizeof(bt_topk_rec),
+                              hipMemcpyDeviceToHost, e->tstream));
+        HIPCHK(hipMemcpyAsync(h + kTopkMax + 1, e->d_ntr[e->cur].p, sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, e->tstream));
+        HIPCHK(hipEventRecord(e->slot_ev[slot], e->tstream));
+        HIPCHK(hipEventRecord(e->ev_tdone[e->cur], e->tstream));  // buffer readers now end here
+        e->slot_armed[slot] = true;
+        return 0;
+    })
+}
+
+int32_t bt_topk_fetch_wait(bt_engine* e, int32_t slot, bt_topk_rec* out, int32_t k,
+                           int64_t* n_trades) {
+    ABI_GUARD(-1, {
+        if (!e || slot < 0 || slot > 1 || !out || k <= 0) throw HipFail{"bad arguments"};
+        if (!e->slot_armed[slot]) throw HipFail{"no fetch pending on this slot"};
+        activate(e);
+        HIPCHK(hipEventSynchronize(e->slot_ev[slot]));
+        const bt_topk_rec* h = e->h_slot[slot];
+        int32_t n = 0;
+        memcpy(&n, h, sizeof n);
+        if (n < 0)
+            throw HipFail{"device top-k overflow (more than 2048 ties on the selected prefix): "
+                          "re-run and read with bt_read_topk"};
+        const int32_t m = std::min(n, std::min(k, e->cfg.topk));
+        std::copy(h + 1, h + 1 + m, out);
+        if (n_trades) {
+            unsigned long long t = 0;
+            memcpy(&t, h + kTopkMax + 1, sizeof t);
+            *n_trades = (int64_t)t;
+        }
+        return m;
+    })
+}
+
 int32_t bt_read_stats(bt_engine* e, bt_stats* out) {
     ABI_GUARD(-1, {
         if (!e || !out) throw HipFail{"bad arguments"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         bt_stats st{};
         st.n_symbols = (int64_t)e->syms.size();
         st.n_params = e->P;
         for (const SymDesc& s : e->syms) st.bar_evals += (int64_t)s.bars * e->P;
         if (e->ran) {
             unsigned long long n = 0;
-            HIPCHK(hipMemcpy(&n, e->d_ntr.p, sizeof n, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&n, e->d_ntr[e->cur].p, sizeof n, hipMemcpyDeviceToHost));
             st.trades = (int64_t)n;
         }
         *out = st;
@@ -639,7 +733,7 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n) 
         const SymDesc& sd = e->syms[sym_index];
         if (n > sd.bars) throw HipFail{"n exceeds bars"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_c.p + sd.off, (size_t)n * 4, hipMemcpyDeviceToHost));
         return 0;
     })
@@ -649,7 +743,7 @@ int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n) {
     ABI_GUARD(-1, {
         if (!e || !out || n < 0 || n > 32 || !e->d_dbg.p) throw HipFail{"no debug stamps"};
         activate(e);
-        HIPCHK(hipStreamSynchronize(e->stream));
+        sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_dbg.p, (size_t)n * 8, hipMemcpyDeviceToHost));
         return 0;
     })
@@ -740,7 +834,7 @@ int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* 
                              C.data()) != 0)
                 throw HipFail{g_err};
             run_impl(e);
-            HIPCHK(hipStreamSynchronize(e->stream));
+            sync_all(e);
         }
         // 3. one CompleteRequest.data string per job, in job order
         std::vector<bt_summary> res((size_t)e->P);
@@ -748,7 +842,7 @@ int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* 
         for (size_t i = 0; i < n; ++i) {
             std::string s;
             if (ok[i]) {
-                HIPCHK(hipMemcpy(res.data(), e->d_sum.p + k * (size_t)e->P,
+                HIPCHK(hipMemcpy(res.data(), e->d_sum[e->cur].p + k * (size_t)e->P,
                                  (size_t)e->P * sizeof(bt_summary), hipMemcpyDeviceToHost));
                 s = fmt_job(res.data(), e->P);
                 outs[i].status = 0;

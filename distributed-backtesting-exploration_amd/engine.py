@@ -109,6 +109,8 @@ def lib():
     L.bt_read_trades.argtypes = [P, P, C.c_size_t]
     L.bt_read_topk.argtypes = [P, P, C.c_int32]
     L.bt_read_stats.argtypes = [P, C.POINTER(_Stats)]
+    L.bt_topk_fetch_async.argtypes = [P, C.c_int32]
+    L.bt_topk_fetch_wait.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(C.c_int64)]
     L.bt_read_close.argtypes = [P, C.c_int32, P, C.c_int32]
     L.bt_kernel_timing.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                    C.POINTER(C.c_char_p)]
@@ -304,6 +306,19 @@ class Engine:
         out = np.zeros(k, TOPK_DTYPE)
         m = _check(lib().bt_read_topk(self._h, out.ctypes.data, k))
         return out[:m]
+
+    def topk_fetch_async(self, slot: int) -> None:
+        """Enqueue the read-back of the last run's top-k and trade count into pinned slot 0/1
+        (no host wait): the next run can be enqueued before these records are consumed."""
+        _check(lib().bt_topk_fetch_async(self._h, slot))
+
+    def topk_fetch_wait(self, slot: int, k=None) -> tuple:
+        """Wait for the slot's read-back; returns (top-k records, trades of that run)."""
+        k = k or self.topk
+        out = np.zeros(k, TOPK_DTYPE)
+        n = C.c_int64(0)
+        m = _check(lib().bt_topk_fetch_wait(self._h, slot, out.ctypes.data, k, C.byref(n)))
+        return out[:m], int(n.value)
 
     def stats(self) -> dict:
         st = _Stats()

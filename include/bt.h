@@ -150,6 +150,15 @@ int32_t bt_read_sums(bt_engine* e, bt_sums* out, size_t n);             /* parit
 int32_t bt_read_trades(bt_engine* e, bt_trade* out, size_t n);          /* n = sym x param x cap */
 int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k);        /* returns count */
 int32_t bt_read_stats(bt_engine* e, bt_stats* out);
+/* Pipelined read-back of the last run's top-k and trade count: bt_topk_fetch_async enqueues
+ * the device-to-host copy into pinned slot 0 or 1 behind the run (no host wait), so the next
+ * bt_run can be enqueued before this run's records are consumed; bt_topk_fetch_wait waits for
+ * that copy only and returns the record count (or -1 if the device selection overflowed — more
+ * than 2,048 records tie on the selected key prefix — in which case re-run and use
+ * bt_read_topk, which finishes on the host). A slot stays valid until its next fetch. */
+int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot);
+int32_t bt_topk_fetch_wait(bt_engine* e, int32_t slot, bt_topk_rec* out, int32_t k,
+                           int64_t* n_trades);
 /* Read back the synthetic/uploaded close column of one symbol (tests). */
 int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n);
 /* Average device time of the dominant kernel (BT_FLAG_TIMING), and how many launches. */

@@ -292,3 +292,24 @@ def test_spec_maximum_windows(strategy):
             where = f"{strategy} max windows sym {s} {grid.param(p)}"
             compare_summary(got[s, p], orc[p], where)
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_pipelined_topk_fetch():
+    """bench.py's pipelining: run i+1 is enqueued before run i's top-k is read; each slot must
+    hold its own run's records and trade count (same as the synchronous read of that run)."""
+    grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
+    with D.Engine(grid, topk=20) as e:
+        refs = []
+        for first in (0, 300):
+            e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
+            e.run()
+            refs.append((e.read_topk(), e.stats()["trades"]))
+        e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
+        e.run()
+        e.topk_fetch_async(0)
+        e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)   # stream-ordered after slot 0's copy
+        e.run()
+        e.topk_fetch_async(1)
+        for slot, (top, trades) in enumerate(refs):
+            got, n = e.topk_fetch_wait(slot)
+            assert got.tolist() == top.tolist() and n == trades
