@@ -35,6 +35,9 @@ from dbx_amd import parallel as PAR  # noqa: E402
 
 SEED, TOPK = 0x5EED, 100
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue ceiling: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction
+# (MI355X_MICROARCH.md per-instruction constants: v_fma_f32 wave64 = 2 cycles on SIMD-32)
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
 
 # per-GPU shard of each BASELINE config: grid, symbols, bars, bar frequency, annualization,
 # and the SURVEY.md §8(d) byte-model terms c (OHLC columns consumed) and W (indicator series)
@@ -113,6 +116,27 @@ def load_traffic(config):
         return float(v["hbm_read_bytes"] + v["hbm_write_bytes"])
     except Exception:
         return None
+
+
+def load_valu_insts(config):
+    """VALU wave-instructions per launch of the dominant kernel (PMC SQ_INSTS_VALU) from the
+    committed rocprofv3 summaries: the kernels are VALU-issue bound, not HBM bound."""
+    try:
+        if config == 2:
+            d = json.load(open(os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")))
+            return float(d["sq"]["SQ_INSTS_VALU"])
+        d = json.load(open(os.path.join(ROOT, "profiles", "r01_configs", "configs.json")))
+        return float(d[f"config{config}"]["pmc"]["SQ_INSTS_VALU"])
+    except Exception:
+        return None
+
+
+def valu_issue(insts, kernel_s):
+    if insts is None:
+        return None
+    achieved = insts / kernel_s / 1e9
+    return {"insts_per_launch": insts, "achieved": achieved, "peak": VALU_PEAK_GINST,
+            "unit": "Ginst/s", "frac": achieved / VALU_PEAK_GINST}
 
 
 def main():
@@ -226,6 +250,9 @@ def main():
                          "traffic": traffic,
                          "kernel": kname, "kernel_avg_ms": kavg_s * 1e3,
                          "alg_bytes_per_launch": alg},
+            # the bound that actually limits the fused kernels: VALU issue (PMC instruction
+            # count per launch from profiles/, over the live kernel time)
+            "valu_issue": valu_issue(load_valu_insts(args.config), kavg_s),
             "trades_per_step": stats["trades"],
             "top1": {"sharpe": float(top[0]["sharpe"]), "sym": int(top[0]["sym"]),
                      "param": int(top[0]["param"])} if len(top) else None,

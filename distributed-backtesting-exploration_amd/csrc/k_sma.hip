@@ -425,12 +425,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
         // (tile k+1) on every wave, balanced dynamically
         if ((helper || dstw) && k + 2 < ntiles && !(g.ablate & 1)) {
+            // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
+            if (!(g.ablate & 32)) __builtin_amdgcn_s_setprio(2);
             const int s = (k + 2) % kStages;
             if (helper)
                 stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
                            qls + s * 2 * kTile, cy);
             if (dstw || dsth) stage_dst(cpre, lane, dst + s * kDstLevels * kTile);
             cpre = load_close(crow, B, t0 + 3 * kTile + lane);
+            __builtin_amdgcn_s_setprio(0);
         }
         BT_STAMP(0)
         // ---- stage 3 (tile k)
