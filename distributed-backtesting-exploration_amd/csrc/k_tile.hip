@@ -189,8 +189,15 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         __builtin_amdgcn_s_setprio(0);
     };
 
+    // with task-only waves present the parameter waves only walk: the walk is the per-tile
+    // critical path (config 3: ~3.7k of ~4.9k cycles per tile on the parameter wave)
+    const bool walk_only = nextra >= 2;
+    const bool no_tasks = walk_only && wave < npw;
+    const int ngrab = nwaves - (walk_only ? npw : 0);
+
     // condition words of tile T, tasks grabbed dynamically (round T), lane = bar
     auto flags = [&](int T) {
+        if (no_tasks) return;
         const int s = T % kTileStages, t = T * kTile + lane;
         const int32_t cl = cts[s * kTile + lane];
         const double cd = (double)cl, lhs = cd * 10000.0;
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const double* E = ebuf + (T & 1) * estage;
         const int ptop = ring_pos(T, lane, R);
         const uint64_t P1t = r1[ptop], P2t = r2[ptop];
-        const uint32_t base = (uint32_t)T * (uint32_t)(ntask + nwaves);
+        const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
         while (o < (uint32_t)ntask) {
@@ -260,7 +267,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             cpre = ldc(crow, B, t0 + 3 * kTile + lane, 0);
         }
         if (STAMPS) sa.mark(0);
-        if (active) {
+        if (active && !(g.ablate & 8)) {
+            __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
@@ -304,8 +312,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             }
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
+            __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles) flags(k + 1);
+        if (k + 1 < ntiles && !(g.ablate & 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
@@ -561,6 +570,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         }
         if (STAMPS) sa.mark(0);
         if (active && !(g.ablate & 8)) {
+            __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
@@ -626,6 +636,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             }
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
+            __builtin_amdgcn_s_setprio(0);
         }
         if (k + 1 < ntiles && !(g.ablate & 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
@@ -640,7 +651,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 // ----------------------------------------------------------------------------- launchers
 // Extra task-only waves per block (they take condition-word tasks only). The EMA kernel has one
 // parameter wave per symbol on config 3 and is latency-bound at ~1.5 waves per SIMD: two extra
-// waves take 4.96 -> 3.68 ms. The Bollinger kernel already runs 5 waves x 2 blocks per CU and
+// waves take 4.96 -> 3.68 ms, four (with the parameter wave walking only, at raised priority)
+// 3.37 ms; six no longer fit two blocks per CU (5.0 ms). The Bollinger kernel already runs 5 waves x 2 blocks per CU and
 // its 122 VGPRs cap a CU at 16 waves: extra waves only cost it (12.4 -> 12.9 ms with 2).
 static int tile_param_waves(int need, int cap) {
     int pw = std::min(need, cap);
@@ -660,7 +672,7 @@ hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* clo
                           const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
     const int pw = tile_param_waves((g.n_params + 63) / 64, 1024 / 64 - 2);
-    const int xw = tile_extra_waves(pw + 2, 2);
+    const int xw = tile_extra_waves(pw + 2, 4);
     const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
     const dim3 block(64 * (pw + 2 + xw));
     const size_t lds = ema_lds_bytes(g);
