@@ -106,7 +106,7 @@ __device__ __forceinline__ uint64_t bits_from(int cur) { return cur < kTile ? (~
 template <bool PARITY, bool STAMPS>
 __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
-                                                        Grid g, Out out, int nextra) {
+                                                        Grid g, Out out, int nextra, int lpw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nsp = g.na, nol = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(0, R, nsp, nol);
@@ -126,13 +126,14 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const bool helperA = wave == npw, helperB = wave == npw + 1;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
-    const int j = blockIdx.y * npw * 64 + tid;
-    const bool active = wave < npw && j < P;
+    // lpw parameter lanes per parameter wave (64, or fewer for shorter max-over-lanes walks)
+    const int j = (blockIdx.y * npw + wave) * lpw + lane;
+    const bool active = wave < npw && lane < lpw && j < P;
     const int pj = active ? j : 0;
     const int i_n = pj / nol, i_w = pj % nol;
     const int warm = max(g.a[i_n], g.b[i_w]) - 1;
     const int32_t* crow = close + sd.off;
-    const int nword = 4 * nsp + 2 * nol, ntask = nsp + nol;
+    const int nword = 4 * nsp + 2 * nol, ntask = max(nsp, nol);
     const int estage = nsp * kEStride;
 
     for (int o = tid; o < nol; o += blockDim.x) win[o] = g.b[o];
@@ -142,6 +143,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     }
     double alpha = 0.0, ema = 0.0;
     if (helperB && lane < nsp) alpha = 2.0 / ((double)g.a[lane] + 1.0);
+    const int winreg = lane < nol ? g.b[lane] : 1;  // OLS window lengths, lane = window
     const double lo_mult = (double)(10000 - g.band_bps), hi_mult = (double)(10000 + g.band_bps);
     __syncthreads();
 
@@ -195,7 +197,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const bool no_tasks = walk_only && wave < npw;
     const int ngrab = nwaves - (walk_only ? npw : 0);
 
-    // condition words of tile T, tasks grabbed dynamically (round T), lane = bar
+    // condition words of tile T, tasks grabbed dynamically (round T), lane = bar. Task o pairs
+    // span o with OLS window o (either may be absent): both rows' LDS reads are issued together,
+    // and the window length comes from a register (winreg, lane = window), so a task costs one
+    // dependent LDS round trip after its grab.
     auto flags = [&](int T) {
         if (no_tasks) return;
         const int s = T % kTileStages, t = T * kTile + lane;
@@ -210,8 +215,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 #pragma unroll 1
         while (o < (uint32_t)ntask) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
-            if ((int)o < nsp) {  // span: entry / exit conditions against the EMA
-                const double e = E[o * kEStride + lane];
+            const bool hs = (int)o < nsp, ho = (int)o < nol;  // wave-uniform
+            const int Wn = nol <= 64 ? __builtin_amdgcn_readlane(winreg, (int)o & 63) : win[o];
+            const int pj = ring_back(ptop, Wn, R);
+            const double e = hs ? E[o * kEStride + lane] : 0.0;
+            const uint64_t r1j = ho ? r1[pj] : 0, r2j = ho ? r2[pj] : 0;
+            if (hs) {  // span: entry / exit conditions against the EMA
                 const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
                 const uint64_t wx = __ballot(cd >= e), wy = __ballot(cd <= e);
                 if (lane == 0) {
@@ -220,19 +229,17 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     Wd[4 * o + 2] = wx;
                     Wd[4 * o + 3] = wy;
                 }
-            } else {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
-                const int ow = (int)o - nsp;
-                const int Wn = win[ow];
+            }
+            if (ho) {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
                 const int jj = t + 1 - Wn;
                 const bool valid = jj >= 0 && t < B;
-                const int pj = ring_back(ptop, Wn, R);
-                const uint64_t S = P1t - r1[pj];
-                const uint64_t Tq = (P2t - r2[pj]) - (uint64_t)(int64_t)jj * S;
+                const uint64_t S = P1t - r1j;
+                const uint64_t Tq = (P2t - r2j) - (uint64_t)(int64_t)jj * S;
                 const int64_t N = (int64_t)(2 * Tq - (uint64_t)(Wn - 1) * S);
                 const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
                 if (lane == 0) {
-                    Wd[4 * nsp + 2 * ow] = wp;
-                    Wd[4 * nsp + 2 * ow + 1] = wn;
+                    Wd[4 * nsp + 2 * o] = wp;
+                    Wd[4 * nsp + 2 * o + 1] = wn;
                 }
             }
             o = grab_value(vn) - base;
@@ -396,7 +403,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          const int32_t* __restrict__ high,
                                                          const int32_t* __restrict__ low,
                                                          const int32_t* __restrict__ close,
-                                                         Grid g, Out out, int nextra) {
+                                                         Grid g, Out out, int nextra, int lpw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(1, R, nw, nk);
@@ -417,8 +424,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const bool helper = wave == npw;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
-    const int j = blockIdx.y * npw * 64 + tid;
-    const bool active = wave < npw && j < P;
+    const int j = (blockIdx.y * npw + wave) * lpw + lane;
+    const bool active = wave < npw && lane < lpw && j < P;
     // lanes run k-major (lane j -> (ik, iw, isl, itp)) while results keep the param order
     // ((iw * nk + ik) * nsl + isl) * ntp + itp: a wave then holds one z threshold, and the
     // threshold sets most of a lane's trade rate, so the walk (a wave iterates the maximum
@@ -652,12 +659,19 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 // Extra task-only waves per block (they take condition-word tasks only). The EMA kernel has one
 // parameter wave per symbol on config 3 and is latency-bound at ~1.5 waves per SIMD: two extra
 // waves take 4.96 -> 3.68 ms, four (with the parameter wave walking only, at raised priority)
-// 3.37 ms; six no longer fit two blocks per CU (5.0 ms). The Bollinger kernel already runs 5 waves x 2 blocks per CU and
+// 3.32 ms, five 3.20 ms (8 waves: two blocks per CU still fit); six no longer fit two blocks per
+// CU (5.0 ms). The Bollinger kernel already runs 5 waves x 2 blocks per CU and
 // its 122 VGPRs cap a CU at 16 waves: extra waves only cost it (12.4 -> 12.9 ms with 2).
 static int tile_param_waves(int need, int cap) {
     int pw = std::min(need, cap);
     if (const char* v = getenv("BT_PW")) pw = std::max(1, std::min(atoi(v), pw));  // tuning aid
     return pw;
+}
+
+static int tile_lanes_per_wave() {
+    int l = 64;
+    if (const char* v = getenv("BT_LPW")) l = std::max(1, std::min(atoi(v), 64));  // tuning aid
+    return l;
 }
 
 static int tile_extra_waves(int used, int x) {
@@ -671,17 +685,18 @@ size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = tile_param_waves((g.n_params + 63) / 64, 1024 / 64 - 2);
-    const int xw = tile_extra_waves(pw + 2, 4);
-    const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
+    const int lpw = tile_lanes_per_wave();
+    const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 2);
+    const int xw = tile_extra_waves(pw + 2, 5);
+    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
     const dim3 block(64 * (pw + 2 + xw));
     const size_t lds = ema_lds_bytes(g);
     if (g.ablate & 64)
-        hipLaunchKernelGGL((ema_tile_kernel<false, true>), grid, block, lds, st, syms, close, g, out, xw);
+        hipLaunchKernelGGL((ema_tile_kernel<false, true>), grid, block, lds, st, syms, close, g, out, xw, lpw);
     else if (parity)
-        hipLaunchKernelGGL((ema_tile_kernel<true, false>), grid, block, lds, st, syms, close, g, out, xw);
+        hipLaunchKernelGGL((ema_tile_kernel<true, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
     else
-        hipLaunchKernelGGL((ema_tile_kernel<false, false>), grid, block, lds, st, syms, close, g, out, xw);
+        hipLaunchKernelGGL((ema_tile_kernel<false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
     return hipGetLastError();
 }
 
@@ -689,17 +704,18 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
                        hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const int pw = tile_param_waves((g.n_params + 63) / 64, 1024 / 64 - 1);
+    const int lpw = tile_lanes_per_wave();
+    const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 1);
     const int xw = tile_extra_waves(pw + 1, 0);
-    const dim3 grid(n_sym, (g.n_params + 64 * pw - 1) / (64 * pw));
+    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
     const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
     if (g.ablate & 64)
-        hipLaunchKernelGGL((boll_tile_kernel<false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw);
+        hipLaunchKernelGGL((boll_tile_kernel<false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
     else if (parity)
-        hipLaunchKernelGGL((boll_tile_kernel<true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw);
+        hipLaunchKernelGGL((boll_tile_kernel<true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
     else
-        hipLaunchKernelGGL((boll_tile_kernel<false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
     return hipGetLastError();
 }
 
