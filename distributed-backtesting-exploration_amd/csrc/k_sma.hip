@@ -278,7 +278,7 @@ __device__ __forceinline__ void sma_open(SmaAcct& a, int b, int t, int32_t cx, i
 // The tile's flips F (bar order). Sharpe partials: a close adds +pos * QL[b], an open subtracts
 // np * QL[b] (a reversal adds 2 pos QL[b]); the squared sum changes only on the first entry
 // (-Q2L[b]) and the forced exit (+Q2L[b]).
-template <bool PARITY>
+template <bool PARITY, bool ONE_TRIP>
 __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl, uint64_t LONG,
                                           const int32_t* cT, const int64_t* ql, const Agg* D,
                                           bt_trade* tr, int cap) {
@@ -301,9 +301,28 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     while (F) {
         const int b = __builtin_ctzll(F);
         F &= F - 1;
-        const Agg seg = dst_query_bf(D, a.sb, b);  // issued first: addresses need only b
-        const int32_t cx = cT[b];
-        alt = (uint64_t)ql[b] - alt;
+        Agg seg;
+        int32_t cx;
+        uint64_t qb;
+        if (ONE_TRIP) {
+            // all four LDS reads of the iteration issued before one wait: pays at low occupancy
+            // (config 5's one 16-wave block per CU: 157.7 -> 152.1 ms), costs ~1 % at config 2's
+            // six waves per SIMD, where the compiler's two round trips are hidden anyway
+            const unsigned xs = (unsigned)(a.sb ^ b);
+            const int lv = xs ? 31 - __builtin_clz(xs) : 0;
+            const Agg d1 = D[lv * kTile + a.sb], d2 = D[lv * kTile + b];
+            cx = cT[b];
+            qb = (uint64_t)ql[b];
+            asm volatile("" ::"v"(d1.mx), "v"(d1.mn), "v"(d1.dd), "v"(d1.du), "v"(d2.mx),
+                         "v"(d2.mn), "v"(d2.dd), "v"(d2.du), "v"(cx), "v"((uint32_t)qb),
+                         "v"((uint32_t)(qb >> 32)));
+            seg = agg_merge(d1, d2);
+        } else {
+            seg = dst_query_bf(D, a.sb, b);  // issued first: addresses need only b
+            cx = cT[b];
+            qb = (uint64_t)ql[b];
+        }
+        alt = qb - alt;
         sma_close<PARITY>(a, seg, t0 + b, cx, tr, cap);
         sma_open(a, b, t0 + b, cx, -a.pos);
     }
@@ -318,7 +337,7 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     }
 }
 
-template <bool PARITY, bool STAMPS>
+template <bool PARITY, bool STAMPS, bool ONE_TRIP>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(const SymDesc* __restrict__ syms,
                                                    const int32_t* __restrict__ close, Grid g,
                                                    Out out, int dedicated) {
@@ -522,7 +541,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                 asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
                 Fw = 0;
             }
-            sma_flips<PARITY>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
+            sma_flips<PARITY, ONE_TRIP>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
             BT_STAMP(4)
             if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
                 a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
@@ -597,12 +616,19 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     const dim3 grid(n_sym, sh.gy), block(sh.block);
     size_t lds = sma_lds_bytes(g);
     if (g.ablate & 128) lds = std::max(lds, (size_t)(g.ablate & 256 ? 80 : 60) * 1024);  // occupancy probe
+    // blocks of more than 8 waves (config 5: one 16-wave block per CU) hide little LDS latency:
+    // their reversal loop issues all of an iteration's reads before one wait
+    const bool one_trip = sh.block > 512;
     if (g.ablate & 64)
-        hipLaunchKernelGGL((sma_kernel<false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+    else if (parity && one_trip)
+        hipLaunchKernelGGL((sma_kernel<true, false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity)
-        hipLaunchKernelGGL((sma_kernel<true, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<true, false, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+    else if (one_trip)
+        hipLaunchKernelGGL((sma_kernel<false, false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else
-        hipLaunchKernelGGL((sma_kernel<false, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<false, false, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     return hipGetLastError();
 }
 

@@ -15,7 +15,8 @@ from typing import Sequence
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libbt.so")
+# BT_LIB (tuning aid): another in-tree build of the library, e.g. libbt_base.so for an A/B
+LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("BT_LIB", "libbt.so")))
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 BT_SMA_CROSS, BT_EMA_OLS, BT_BOLL = 1, 2, 3
