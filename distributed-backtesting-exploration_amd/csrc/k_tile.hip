@@ -486,15 +486,21 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         }
     };
 
+    // with two or more task-only waves the parameter waves only walk (at raised priority)
+    const bool walk_only = nextra >= 2;
+    const bool no_tasks = walk_only && wave < npw;
+    const int ngrab = nwaves - (walk_only ? npw : 0);
+
     // condition words of tile T, windows grabbed dynamically (round T), lane = bar
     auto flags = [&](int T) {
+        if (no_tasks) return;
         const int s = T % kTileStages, t = T * kTile + lane;
         const int64_t c = cts[s * kTile + lane];
         uint64_t* Wd = words + (T & 1) * nword;
         const int ptop = ring_pos(T, lane, R);
         const uint64_t P1t = r1[ptop];
         const unsigned __int128 P2t = r2[ptop];
-        const uint32_t base = (uint32_t)T * (uint32_t)(nw + nwaves);
+        const uint32_t base = (uint32_t)T * (uint32_t)(nw + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
         while (o < (uint32_t)nw) {
@@ -660,8 +666,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 // parameter wave per symbol on config 3 and is latency-bound at ~1.5 waves per SIMD: two extra
 // waves take 4.96 -> 3.68 ms, four (with the parameter wave walking only, at raised priority)
 // 3.32 ms, five 3.20 ms (8 waves: two blocks per CU still fit); six no longer fit two blocks per
-// CU (5.0 ms). The Bollinger kernel already runs 5 waves x 2 blocks per CU and
-// its 122 VGPRs cap a CU at 16 waves: extra waves only cost it (12.4 -> 12.9 ms with 2).
+// CU (5.0 ms). The Bollinger kernel runs 5 waves x 2 blocks per CU and its ~120 VGPRs cap a
+// CU at 16 waves: two task-only waves, with the parameter waves then walking only, take config 4
+// 12.3 -> 12.0 ms (250 symbols: 9.95 -> 9.76 ms); four no longer fit two blocks (19.4 ms).
 static int tile_param_waves(int need, int cap) {
     int pw = std::min(need, cap);
     if (const char* v = getenv("BT_PW")) pw = std::max(1, std::min(atoi(v), pw));  // tuning aid
@@ -706,7 +713,7 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     if (n_sym <= 0) return hipSuccess;
     const int lpw = tile_lanes_per_wave();
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 1);
-    const int xw = tile_extra_waves(pw + 1, 0);
+    const int xw = tile_extra_waves(pw + 1, 2);
     const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
     const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
