@@ -270,6 +270,26 @@ def test_sma_block_shapes(nf, ns):
             compare_summary(got[s, p], orc[s, p], f"shape {nf}x{ns} sym {s} param {p}")
 
 
+def test_sma_large_block_trades_parity():
+    """Blocks of more than 8 waves take the one-round-trip reversal loop (k_sma.hip ONE_TRIP):
+    its trade lists in parity mode, a 16-wave grid (P = 1,024) and a 10-wave one (P = 600)."""
+    for nf, ns in ((32, 32), (20, 30)):
+        grid = D.Grid.sma(np.arange(1, nf + 1) * 2, np.arange(1, ns + 1) * 7 + 3,
+                          annualization=252)
+        syms, bars = [11, 12], 900
+        o, h, lo, c = _gen(0x5EED, syms, bars, 0)
+        with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+            e.load_synthetic(0x5EED, syms[0], len(syms), bars, D.BT_DAILY)
+            e.run()
+            got, tr = e.summaries(), e.trades()
+        for i in range(len(syms)):
+            orc, otr = oracle_row("sma", grid, (o[i], h[i], lo[i], c[i]), 252, CAP)
+            for p in range(grid.n_params):
+                where = f"{nf}x{ns} sym {syms[i]} param {grid.param(p)}"
+                compare_summary(got[i, p], orc[p], where)
+                compare_trades(tr[i, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
 @pytest.mark.parametrize("strategy", ["sma", "ema_ols", "boll"])
 def test_spec_maximum_windows(strategy):
     """Windows up to the spec's 4,096 bars (docs/oracle_spec.md §3: w <= 4096 keeps window
