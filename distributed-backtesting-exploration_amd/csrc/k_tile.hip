@@ -32,6 +32,11 @@ namespace bt {
 namespace {
 
 constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflict-free columns
+// Bollinger per-stage low/high staging (int32): lows[64], highs[64], 8 block minima of the lows
+// then 8 block maxima of the highs, and per bar the minimum low / maximum high from that bar to
+// the end of its 8-bar block (SL/TP first-passage search)
+constexpr int kLH = 4 * kTile + 16;
+constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16;
 
 struct TileLds {
     size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, ctr, total;
@@ -48,7 +53,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
     L.ql = take((size_t)kTileStages * 2 * kTile * 8);
     L.dst = take((size_t)kTileStages * kDstLevels * kTile * sizeof(Agg));
     if (kind == 1) {
-        L.stl = take((size_t)kTileStages * (2 * kTile + 16) * 4);  // lows, highs, block extrema
+        L.stl = take((size_t)kTileStages * kLH * 4);  // lows, highs, block and in-block suffix extrema
         L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
         L.words = take((size_t)2 * (2 * na * nb + 2 * na) * 8);
         L.win = take((size_t)na * 4);
@@ -339,7 +344,6 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 //           from an LDS counter (z tests in fp64 with an exact int128 fallback);
 //   parameter waves, tile k: one trade per loop iteration (entry at the first z signal, exit at
 //           the first of SL/TP / signal / forced), O(1) accounting per trade.
-constexpr int kLH = 2 * kTile + 16;  // per stage: lows[64], highs[64], block min[8], block max[8]
 constexpr int kMaxK = 8;             // z thresholds per window (engine-validated)
 
 // 8-bit mask of v_j > X over a (4+4)-int32 group, bit j = element j: the sign bit of X - v_j
@@ -367,27 +371,33 @@ __device__ __forceinline__ void pin4(const int4& v) {
 }
 
 // SL/TP first passage from in-tile bar cur (< 64) of an open trade: xlo = first bar whose low
-// is <= XL, xhi = first bar whose high is > XH1 (64 if none). LO/HI: the tile's 64 lows /
-// highs, BX: 8 block minima of the lows then 8 block maxima of the highs. Two dependent LDS
-// round trips for both searches together: the 8-bar block of `cur` and the block extrema,
-// then the first later block that qualifies.
-__device__ __forceinline__ void sltp_search(const int32_t* LO, const int32_t* HI, const int32_t* BX,
-                                            int cur, int32_t XL, int32_t XH1, int& xlo, int& xhi) {
+// is <= XL, xhi = first bar whose high is > XH1 (64 if none). LH: one stage of the staging
+// (kLH layout). Two dependent LDS round trips for both searches together: round 1 reads the
+// suffix extrema of `cur` within its 8-bar block and the 8 block extrema (one hit test for the
+// rest of the block, 8 for the later blocks), round 2 the 8 bars of the block that holds the
+// first hit (`cur`'s own block from `cur` on, or the first later block that qualifies).
+__device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t XL, int32_t XH1,
+                                            int& xlo, int& xhi) {
     const int cb = cur >> 3;
-    const int4 l0 = ld4(LO + 8 * cb), l1 = ld4(LO + 8 * cb + 4);
-    const int4 h0 = ld4(HI + 8 * cb), h1 = ld4(HI + 8 * cb + 4);
-    const int4 n0 = ld4(BX), n1 = ld4(BX + 4), x0 = ld4(BX + 8), x1 = ld4(BX + 12);
-    pin4(l0); pin4(l1); pin4(h0); pin4(h1); pin4(n0); pin4(n1); pin4(x0); pin4(x1);
-    const uint32_t from = (0xFFu << (cur & 7)) & 0xFFu, after = (0xFEu << cb) & 0xFFu;
-    const uint32_t inL = ~gt8(l0, l1, XL) & from, inH = gt8(h0, h1, XH1) & from;
+    const int32_t sl = LH[kLhSuf + cur], sh = LH[kLhSuf + kTile + cur];
+    const int4 n0 = ld4(LH + kLhBx), n1 = ld4(LH + kLhBx + 4);
+    const int4 x0 = ld4(LH + kLhBx + 8), x1 = ld4(LH + kLhBx + 12);
+    asm volatile("" ::"v"(sl), "v"(sh));
+    pin4(n0); pin4(n1); pin4(x0); pin4(x1);
+    const uint32_t after = (0xFEu << cb) & 0xFFu;
+    const bool inL = sl <= XL, inH = sh > XH1;
     const uint32_t laL = ~gt8(n0, n1, XL) & after, laH = gt8(x0, x1, XH1) & after;
-    const int fL = laL ? __builtin_ctz(laL) : cb, fH = laH ? __builtin_ctz(laH) : cb;
-    const int4 a0 = ld4(LO + 8 * fL), a1 = ld4(LO + 8 * fL + 4);
-    const int4 b0 = ld4(HI + 8 * fH), b1 = ld4(HI + 8 * fH + 4);
+    // block to scan per side (cb when the hit is in cur's block; unused when there is none)
+    const int fL = inL ? cb : (laL ? __builtin_ctz(laL) : cb);
+    const int fH = inH ? cb : (laH ? __builtin_ctz(laH) : cb);
+    const int4 a0 = ld4(LH + 8 * fL), a1 = ld4(LH + 8 * fL + 4);
+    const int4 b0 = ld4(LH + kTile + 8 * fH), b1 = ld4(LH + kTile + 8 * fH + 4);
     pin4(a0); pin4(a1); pin4(b0); pin4(b1);
-    const uint32_t sL = (~gt8(a0, a1, XL) & 0xFFu) | 0x100u, sH = gt8(b0, b1, XH1) | 0x100u;
-    xlo = inL ? 8 * cb + __builtin_ctz(inL) : (laL ? 8 * fL + __builtin_ctz(sL) : kTile);
-    xhi = inH ? 8 * cb + __builtin_ctz(inH) : (laH ? 8 * fH + __builtin_ctz(sH) : kTile);
+    const uint32_t from = (0xFFu << (cur & 7)) & 0xFFu;
+    const uint32_t mL = (~gt8(a0, a1, XL) & (fL == cb ? from : 0xFFu)) | 0x100u;
+    const uint32_t mH = (gt8(b0, b1, XH1) & (fH == cb ? from : 0xFFu)) | 0x100u;
+    xlo = (inL || laL) ? 8 * fL + __builtin_ctz(mL) : kTile;
+    xhi = (inH || laH) ? 8 * fH + __builtin_ctz(mH) : kTile;
 }
 
 // floor(ce * f / 10000) for 0 < ce < 2^31, 0 < f < 2^15 (SL/TP levels, spec §4): the product is
@@ -481,9 +491,21 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             mx = max(mx, __shfl_xor(mx, d, 64));
         }
         if ((lane & 7) == 0) {
-            LH[2 * kTile + (lane >> 3)] = mn;
-            LH[2 * kTile + 8 + (lane >> 3)] = mx;
+            LH[kLhBx + (lane >> 3)] = mn;
+            LH[kLhBx + 8 + (lane >> 3)] = mx;
         }
+        // min low / max high from each bar to the end of its 8-bar block (suffix within the block)
+        int32_t smn = lv, smx = hv;
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) {
+            const int32_t on = __shfl_down(smn, d, 64), ox = __shfl_down(smx, d, 64);
+            if ((lane & 7) + d < 8) {
+                smn = min(smn, on);
+                smx = max(smx, ox);
+            }
+        }
+        LH[kLhSuf + lane] = smn;
+        LH[kLhSuf + kTile + lane] = smx;
     };
 
     // with two or more task-only waves the parameter waves only walk (at raised priority)
@@ -589,7 +611,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int64_t* ql = qls + s * 2 * kTile;
             const Agg* D = dst + s * kDstLevels * kTile;
             const int32_t* LO = lhs_ + s * kLH;
-            const int32_t* HI = LO + kTile;
             const uint64_t* W = words + (k & 1) * nword;
             const uint64_t vm = bar_range_mask(t0, w - 1, B - 2);
             const uint64_t ZL = W[2 * (iw * nk + ik)] & vm, ZH = W[2 * (iw * nk + ik) + 1] & vm;
@@ -625,7 +646,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 int x = sig ? __builtin_ctzll(sig) : kTile;
                 if (bl >= cur && bl < kTile) x = min(x, bl);
                 int xlo, xhi;
-                sltp_search(LO, HI, LO + 2 * kTile, cur, XL, XHm1, xlo, xhi);
+                sltp_search(LO, cur, XL, XHm1, xlo, xhi);
                 const int xs = min(xlo, xhi);
                 int32_t px;
                 Agg st;
