@@ -648,19 +648,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 int xlo, xhi;
                 sltp_search(LO, cur, XL, XHm1, xlo, xhi);
                 const int xs = min(xlo, xhi);
-                int32_t px;
-                Agg st;
-                if (xs < kTile && xs <= x) {
-                    x = xs;
-                    px = (xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1;
-                    const Agg before = x > a.sb ? dst_query_bf(D, a.sb, x - 1) : kAggId;
-                    st = agg_merge(agg_merge(a.agg, before), agg_one(px));
-                } else if (x < kTile) {
-                    px = cT[x];
-                    st = agg_merge(a.agg, dst_query_bf(D, a.sb, x));
-                } else {
-                    break;
-                }
+                const bool hit = xs < kTile && xs <= x;
+                if (!hit && x >= kTile) break;
+                // one path for both exit kinds (no divergence): the trade's closes up to the bar
+                // before an SL/TP fill or up to a signal exit's bar, then the fill price (for a
+                // signal exit that is the last close again, which leaves the aggregate unchanged)
+                if (hit) x = xs;
+                const int qi = hit ? x - 1 : x;  // >= a.sb - 1 (exits come after the entry bar)
+                const int32_t px = hit ? ((xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1) : cT[x];
+                const Agg seg = dst_query_bf(D, a.sb, max(qi, a.sb));
+                const Agg st = agg_merge(agg_merge(a.agg, qi < a.sb ? kAggId : seg), agg_one(px));
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
                 acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
                 a.ps1 += lg ? qx : (uint64_t)0 - qx;
