@@ -614,8 +614,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const uint64_t* W = words + (k & 1) * nword;
             const uint64_t vm = bar_range_mask(t0, w - 1, B - 2);
             const uint64_t ZL = W[2 * (iw * nk + ik)] & vm, ZH = W[2 * (iw * nk + ik) + 1] & vm;
-            const uint64_t DP = W[2 * nw * nk + 2 * iw] & vm, DN = W[2 * nw * nk + 2 * iw + 1] & vm;
-            const int bl = B - 1 - t0;  // forced exit bar (>= 0; in this tile iff < 64)
+            // signal exits with the forced exit at bar B-1 folded in (in this tile iff bl < 64)
+            const int bl = B - 1 - t0;
+            const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;
+            const uint64_t DP = (W[2 * nw * nk + 2 * iw] & vm) | fb;
+            const uint64_t DN = (W[2 * nw * nk + 2 * iw + 1] & vm) | fb;
             int cur = 0;
 #pragma unroll 1
             while (true) {  // one trade (entry and/or exit) per iteration, in bar order
@@ -642,9 +645,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 // exit: first of SL/TP (intrabar, from entry + 1; SL wins a same-bar tie), the
                 // signal exit and the forced exit at B-1 (SL/TP beat both on the same bar)
                 const bool lg = a.pos > 0;
-                const uint64_t sig = (lg ? DP : DN) & bits_from(cur);
+                const uint64_t sig = (lg ? DP : DN) & (~0ULL << cur);  // cur < 64 here
                 int x = sig ? __builtin_ctzll(sig) : kTile;
-                if (bl >= cur && bl < kTile) x = min(x, bl);
                 int xlo, xhi;
                 sltp_search(LO, cur, XL, XHm1, xlo, xhi);
                 const int xs = min(xlo, xhi);
