@@ -387,6 +387,10 @@ __device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t 
     const uint32_t after = (0xFEu << cb) & 0xFFu;
     const bool inL = sl <= XL, inH = sh > XH1;
     const uint32_t laL = ~gt8(n0, n1, XL) & after, laH = gt8(x0, x1, XH1) & after;
+    xlo = xhi = kTile;
+    // round 2 only when some lane of the wave has a hit in the tile (not in a wave's last
+    // iteration, which mostly carries open trades past the tile end)
+    if (!__ballot(inL || inH || laL || laH)) return;
     // block to scan per side (cb when the hit is in cur's block; unused when there is none)
     const int fL = inL ? cb : (laL ? __builtin_ctz(laL) : cb);
     const int fH = inH ? cb : (laH ? __builtin_ctz(laH) : cb);
