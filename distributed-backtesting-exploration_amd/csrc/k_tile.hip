@@ -404,13 +404,12 @@ __device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t 
     xhi = (inH || laH) ? 8 * fH + __builtin_ctz(mH) : kTile;
 }
 
-// floor(ce * f / 10000) for 0 < ce < 2^31, 0 < f < 2^15 (SL/TP levels, spec §4): the product is
-// exact in fp64 (< 2^46); fl(1e-4) and the product add < 2^-19 absolute error and the 2^-16
-// offset keeps the sum inside [n, n + 1) for every remainder 0..9999.
-__device__ __forceinline__ int64_t level_div(int32_t ce, int32_t f) {
-    const double y = ((double)ce * (double)f) * 1e-4;
-    return (int64_t)floor(y + 0x1p-16);
-}
+// SL/TP levels floor(ce * f / 10000) for 0 < ce < 2^31, 0 < f < 2^15 (spec §4), with the
+// per-lane factor g = fl(f * fl(1e-4)) precomputed: y = fl(ce * g) is within 3 * 2^-53 relative
+// (< 2^-18.7 absolute, y < 2^32.7) of ce * f / 10000 = n + r / 10000 (0 <= r <= 9999), so the
+// 2^-16 offset keeps y + 2^-16 inside (n, n + 1) and truncation is the exact floor
+// (tests/test_oracle_golden.py::test_sltp_level_floor checks every f against integer division).
+__device__ __forceinline__ double level_y(double ce, double g) { return ce * g + 0x1p-16; }
 
 template <bool PARITY, bool STAMPS>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
@@ -451,6 +450,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int pj = ((iw * nk + ik) * g.nc + isl) * g.nd + itp;
     const int w = g.a[iw];
     const int32_t sl_bps = g.c[isl], tp_bps = g.d[itp];
+    // level factors (10000 -+ bps) * 1e-4 per side of the trade (level_y)
+    const double gl_long = (double)(10000 - sl_bps) * 1e-4, gl_short = (double)(10000 - tp_bps) * 1e-4;
+    const double gh_long = (double)(10000 + tp_bps) * 1e-4, gh_short = (double)(10000 + sl_bps) * 1e-4;
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
@@ -638,11 +640,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     a.ps2 -= q2x;
                     acct_open(a, t0 + b, b, cx);
                     a.pos = np;
-                    // low-side level: long SL / short TP; high-side: long TP / short SL (< 2^46)
-                    const int64_t xl = level_div(cx, np > 0 ? 10000 - sl_bps : 10000 - tp_bps);
-                    const int64_t xh = level_div(cx, np > 0 ? 10000 + tp_bps : 10000 + sl_bps);
-                    XL = (int32_t)xl;
-                    XHm1 = (int32_t)min(xh - 1, (int64_t)INT32_MAX);
+                    // low-side level: long SL / short TP (< ce); high-side: long TP / short SL
+                    // (may reach 2^31: no high can exceed it then)
+                    const double cd = (double)cx;
+                    const double yl = level_y(cd, np > 0 ? gl_long : gl_short);
+                    const double yh = level_y(cd, np > 0 ? gh_long : gh_short);
+                    XL = (int32_t)yl;
+                    XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
                     cur = b + 1;
                 }
                 if (cur >= kTile) break;

@@ -123,6 +123,27 @@ def test_numpy_restatement_matches_c_fresh():
         assert int(r["pnl"]) == e["pnl"] and int(r["mdd"]) == e["mdd"] and int(r["hash"]) == e["h"]
 
 
+def test_sltp_level_floor():
+    """k_tile.hip level_y: trunc(fl(ce * fl(f * fl(1e-4))) + 2^-16) == floor(ce * f / 10000) (the
+    oracle's integer SL/TP levels, oracle/oracle.c orc_boll) for every factor f = 10000 -+ bps,
+    bps in [0, 9999], at random prices and at prices whose product leaves remainder 0, 1 or 9999
+    (the only places a rounding error could move the truncation) near 2^31."""
+    rng = np.random.default_rng(12)
+    f = np.concatenate([10000 - np.arange(10000), 10000 + np.arange(10000)]).astype(np.int64)
+    g = f.astype(np.float64) * 1e-4
+    ce = np.concatenate([[1, 2, 9999, 10000, 10001, 2 ** 30, 2 ** 31 - 2, 2 ** 31 - 1],
+                         rng.integers(1, 2 ** 31, 40)]).astype(np.int64)
+    y = ce[None, :].astype(np.float64) * g[:, None] + 2.0 ** -16
+    assert np.array_equal(np.trunc(y).astype(np.int64), (ce[None, :] * f[:, None]) // 10000)
+    # adversarial remainders: prices ce = 2^31 - k with ce * f % 10000 in {0, 1, 9999}
+    c = (2 ** 31 - 1 - np.arange(10000, dtype=np.int64))
+    for fi, gi in zip(f[::3], g[::3]):
+        r = (c * fi) % 10000
+        sel = c[(r == 0) | (r == 1) | (r == 9999)]
+        got = np.trunc(sel.astype(np.float64) * gi + 2.0 ** -16).astype(np.int64)
+        assert np.array_equal(got, (sel * fi) // 10000), f"level mismatch f={fi}"
+
+
 def test_biased_reciprocal_floor():
     """k_sma.hip floor_key: trunc(F * key_recip(W)) == floor(F / W) for every window length the
     SMA kernel can hold (W <= 16,384; its LDS ring caps windows near 16,000) and F/W < 2^31,
