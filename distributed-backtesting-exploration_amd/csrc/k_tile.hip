@@ -238,9 +238,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             if (ho) {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
                 const int jj = t + 1 - Wn;
                 const bool valid = jj >= 0 && t < B;
+                // 2 (sum i c_i - jj S) - (w - 1) S with one multiply
                 const uint64_t S = P1t - r1j;
-                const uint64_t Tq = (P2t - r2j) - (uint64_t)(int64_t)jj * S;
-                const int64_t N = (int64_t)(2 * Tq - (uint64_t)(Wn - 1) * S);
+                const int64_t N = (int64_t)(2 * (P2t - r2j) - (uint64_t)(int64_t)(2 * jj + Wn - 1) * S);
                 const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
                 if (lane == 0) {
                     Wd[4 * nsp + 2 * o] = wp;
