@@ -550,9 +550,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                 a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
                 a.ps2 += (uint64_t)ql[2 * kTile - 1];
             }
-            a.s1 += (i128)(int64_t)a.ps1;
-            a.s2 += (i128)(int64_t)a.ps2;
-            a.ps1 = a.ps2 = 0;
+            // fold the return partials into int128 every second tile (and at the last): over
+            // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
+            // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
+            // zero price), so the uint64 partials are exact as int64
+            if ((k & 1) || k + 1 == ntiles) {
+                a.s1 += (i128)(int64_t)a.ps1;
+                a.s2 += (i128)(int64_t)a.ps2;
+                a.ps1 = a.ps2 = 0;
+            }
             BT_STAMP(5)
         }
         if (k + 1 < ntiles && !(g.ablate & 2))
