@@ -457,6 +457,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         BT_STAMP(0)
         // ---- stage 3 (tile k)
         if (active) {
+            // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
+            // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
+            // blocks are ~1 % slower with it)
+            if (ONE_TRIP) __builtin_amdgcn_s_setprio(1);
             const int s = k % kStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
@@ -560,6 +564,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                 a.ps1 = a.ps2 = 0;
             }
             BT_STAMP(5)
+            if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
         }
         if (k + 1 < ntiles && !(g.ablate & 2))
             stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
