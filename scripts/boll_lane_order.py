@@ -77,3 +77,14 @@ for span in (128, 256):
     order = key_order(lambda p: (params[p][1], params[p][0], params[p][2], params[p][3]))
     g = IT[:, order, :].reshape(nsym, P // 64, 64, n)
     print(f"walk span {span} bars, k-major: {g.max(axis=2).sum() / (nsym * T):.2f} per 64-bar block-tile")
+
+# how the measured rate depends on the axes (for a grid-only ordering heuristic)
+r = rate_all.reshape(8, 4, 2, 4).astype(float)
+print("mean rate by w:", np.round(r.mean(axis=(1, 2, 3)), 0))
+print("by k:", np.round(r.mean(axis=(0, 2, 3)), 0), "by sl:", np.round(r.mean(axis=(0, 1, 3)), 0),
+      "by tp:", np.round(r.mean(axis=(0, 1, 2)), 0))
+for name, key in (("k, then sl+tp", lambda p: (params[p][1], params[p][2] + params[p][3])),
+                  ("sl+tp, then k", lambda p: (params[p][2] + params[p][3], params[p][1])),
+                  ("w, then k", lambda p: (params[p][0], params[p][1])),
+                  ("k+w", lambda p: (params[p][1] + params[p][0] / 2, params[p][2]))):
+    print(name, round(cost(key_order(key)), 2))
