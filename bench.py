@@ -58,7 +58,7 @@ def algorithmic_bytes(S, B, P, c=1, W=40):
     return S * B * (8 * c + 16 * W) + 32 * S * P
 
 
-def cpu_baseline(cfg, grid, threads=None, target_thread_s=15.0):
+def cpu_baseline(cfg, grid, threads=None, target_thread_s=25.0):
     """The C oracle (oracle/oracle.c, -O2 -ffp-contract=off) on the first symbols of
     the same workload, sized from a one-symbol probe to ~target_thread_s thread-seconds. SMA
     grids run on the oracle's pthread grid (one symbol per thread); EMA/Bollinger run one
@@ -100,8 +100,8 @@ def cpu_baseline(cfg, grid, threads=None, target_thread_s=15.0):
     evals = n_sym * B * grid.n_params
     return {"value": evals / dt, "unit": "bar-evals/s", "cores": threads, "kind": "port",
             "sample": f"first {n_sym} of the {cfg['S']} shard symbols x {B} bars x "
-                      f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall on "
-                      f"{threads} threads; oracle/oracle.c, gcc -O2 -ffp-contract=off)"}
+                      f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall = "
+                      f"{dt * threads:.1f} thread-s on {threads} threads; oracle/oracle.c, gcc -O2 -ffp-contract=off)"}
 
 
 def load_traffic(config):

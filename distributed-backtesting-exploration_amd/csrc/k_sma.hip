@@ -239,10 +239,11 @@ struct SmaAcct {
 // most one entry from flat, then reversals (a branch-free loop), then at most the forced exit.
 
 // Closes the open trade at in-tile bar b (fill cx = close of bar t = t0 + b).
-template <bool PARITY>
+// MERGE = false: the trade opened in this tile (a.agg is the identity), so seg is its whole path.
+template <bool PARITY, bool MERGE = true>
 __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int32_t cx,
                                           bt_trade* tr, int cap) {
-    const Agg st = agg_merge(a.agg, seg);   // seg: closes [sb, b] of this tile
+    const Agg st = MERGE ? agg_merge(a.agg, seg) : seg;   // seg: closes [sb, b] of this tile
     const bool lg = a.pos > 0;
     const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
     const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
@@ -267,12 +268,49 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int
     a.ntr++;
 }
 
+template <bool RESET_AGG = true>
 __device__ __forceinline__ void sma_open(SmaAcct& a, int b, int t, int32_t cx, int np) {
     a.e = t;
     a.ce = cx;
     a.sb = b;
-    a.agg = kAggId;
+    if (RESET_AGG) a.agg = kAggId;
     a.pos = np;
+}
+
+// One reversal at the lowest flip of F. FIRST: the lane's first reversal of the tile, whose
+// closing trade may carry a path from earlier tiles (a.agg); every later reversal of the tile
+// closes a trade opened at the previous flip, so it skips the merge and leaves a.agg alone
+// (already the identity).
+template <bool PARITY, bool ONE_TRIP, bool FIRST>
+__device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& alt, int t0,
+                                            const int32_t* cT, const int64_t* ql, const Agg* D,
+                                            bt_trade* tr, int cap) {
+    const int b = __builtin_ctzll(F);
+    F &= F - 1;
+    Agg seg;
+    int32_t cx;
+    uint64_t qb;
+    if (ONE_TRIP) {
+        // all four LDS reads of the iteration issued before one wait: pays at low occupancy
+        // (config 5's one 16-wave block per CU: 157.7 -> 152.1 ms), costs ~1 % at config 2's
+        // six waves per SIMD, where the compiler's two round trips are hidden anyway
+        const unsigned xs = (unsigned)(a.sb ^ b);
+        const int lv = xs ? 31 - __builtin_clz(xs) : 0;
+        const Agg d1 = D[lv * kTile + a.sb], d2 = D[lv * kTile + b];
+        cx = cT[b];
+        qb = (uint64_t)ql[b];
+        asm volatile("" ::"v"(d1.mx), "v"(d1.mn), "v"(d1.dd), "v"(d1.du), "v"(d2.mx),
+                     "v"(d2.mn), "v"(d2.dd), "v"(d2.du), "v"(cx), "v"((uint32_t)qb),
+                     "v"((uint32_t)(qb >> 32)));
+        seg = agg_merge(d1, d2);
+    } else {
+        seg = dst_query_bf(D, a.sb, b);  // issued first: addresses need only b
+        cx = cT[b];
+        qb = (uint64_t)ql[b];
+    }
+    alt = qb - alt;
+    sma_close<PARITY, FIRST>(a, seg, t0 + b, cx, tr, cap);
+    sma_open<FIRST>(a, b, t0 + b, cx, -a.pos);
 }
 
 // The tile's flips F (bar order). Sharpe partials: a close adds +pos * QL[b], an open subtracts
@@ -298,34 +336,8 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     // p_k = (-1)^(k-1) p_1 and adds 2 p_k QL[b_k]: an alternating sum, carried as
     // alt_k = QL[b_k] - alt_(k-1), so that sum = 2 p_n alt_n = -2 pos alt after the loop
     uint64_t alt = 0;
-    while (F) {
-        const int b = __builtin_ctzll(F);
-        F &= F - 1;
-        Agg seg;
-        int32_t cx;
-        uint64_t qb;
-        if (ONE_TRIP) {
-            // all four LDS reads of the iteration issued before one wait: pays at low occupancy
-            // (config 5's one 16-wave block per CU: 157.7 -> 152.1 ms), costs ~1 % at config 2's
-            // six waves per SIMD, where the compiler's two round trips are hidden anyway
-            const unsigned xs = (unsigned)(a.sb ^ b);
-            const int lv = xs ? 31 - __builtin_clz(xs) : 0;
-            const Agg d1 = D[lv * kTile + a.sb], d2 = D[lv * kTile + b];
-            cx = cT[b];
-            qb = (uint64_t)ql[b];
-            asm volatile("" ::"v"(d1.mx), "v"(d1.mn), "v"(d1.dd), "v"(d1.du), "v"(d2.mx),
-                         "v"(d2.mn), "v"(d2.dd), "v"(d2.du), "v"(cx), "v"((uint32_t)qb),
-                         "v"((uint32_t)(qb >> 32)));
-            seg = agg_merge(d1, d2);
-        } else {
-            seg = dst_query_bf(D, a.sb, b);  // issued first: addresses need only b
-            cx = cT[b];
-            qb = (uint64_t)ql[b];
-        }
-        alt = qb - alt;
-        sma_close<PARITY>(a, seg, t0 + b, cx, tr, cap);
-        sma_open(a, b, t0 + b, cx, -a.pos);
-    }
+    if (F) sma_reverse<PARITY, ONE_TRIP, true>(a, F, alt, t0, cT, ql, D, tr, cap);
+    while (F) sma_reverse<PARITY, ONE_TRIP, false>(a, F, alt, t0, cT, ql, D, tr, cap);
     a.ps1 += a.pos > 0 ? (uint64_t)0 - (alt << 1) : alt << 1;
     if (FX) {  // flat after bar B-1 (only set when a position is open before it)
         const int b = bl;
