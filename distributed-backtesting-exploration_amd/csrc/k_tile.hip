@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "tile_common.h"
 
 namespace bt {
@@ -293,12 +295,15 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             const int bl = B - 1 - t0;
             const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;  // forced exit (bl >= 0)
             int cur = 0;
-#pragma unroll 1
-            while (true) {  // one trade (entry and/or exit) per iteration, in bar order
+            // one trade (entry and/or exit) per call, in bar order; false when the tile is done.
+            // Only the first trade of the tile can start open (a position carried in, path in
+            // a.agg): later ones start flat and their path lies in this tile (no merge)
+            auto trade = [&](auto first_tag) -> bool {
+                constexpr bool FIRST = decltype(first_tag)::value;
                 if (STAMPS) sa.count(3);
-                if (a.pos == 0) {
+                if (!FIRST || a.pos == 0) {
                     const uint64_t m = (Aw | Bw) & bits_from(cur);
-                    if (m == 0) break;
+                    if (m == 0) return false;
                     const int b = __builtin_ctzll(m);
                     const int np = ((Aw >> b) & 1) ? 1 : -1;
                     const int32_t cx = cT[b];
@@ -310,17 +315,24 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     cur = b + 1;
                 }
                 const uint64_t m = ((a.pos > 0 ? Xw : Yw) | fb) & bits_from(cur);
-                if (m == 0) break;
+                if (m == 0) return false;
                 const int x = __builtin_ctzll(m);
                 const int32_t cx = cT[x];
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                const Agg st = agg_merge(a.agg, dst_query_bf(D, a.sb, x));
+                const Agg seg = dst_query_bf(D, a.sb, x);
+                const Agg st = FIRST ? agg_merge(a.agg, seg) : seg;
                 const bool lg = a.pos > 0;
                 acct_close<PARITY>(a, t0 + x, cx, st, tr, cap);
                 a.ps1 += lg ? qx : (uint64_t)0 - qx;
                 a.ps2 += q2x;
                 a.pos = 0;
                 cur = x + 1;
+                return true;
+            };
+            if (trade(std::true_type{})) {
+#pragma unroll 1
+                while (trade(std::false_type{})) {
+                }
             }
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
@@ -626,12 +638,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const uint64_t DP = (W[2 * nw * nk + 2 * iw] & vm) | fb;
             const uint64_t DN = (W[2 * nw * nk + 2 * iw + 1] & vm) | fb;
             int cur = 0;
-#pragma unroll 1
-            while (true) {  // one trade (entry and/or exit) per iteration, in bar order
+            // one trade (entry and/or exit) per call, in bar order; false when the tile is done.
+            // Only the first trade of the tile can start open (path carried in a.agg)
+            auto trade = [&](auto first_tag) -> bool {
+                constexpr bool FIRST = decltype(first_tag)::value;
                 if (STAMPS) sa.count(3);
-                if (a.pos == 0) {
+                if (!FIRST || a.pos == 0) {
                     const uint64_t m = (ZL | ZH) & bits_from(cur);
-                    if (m == 0) break;
+                    if (m == 0) return false;
                     const int b = __builtin_ctzll(m);
                     const int np = ((ZL >> b) & 1) ? 1 : -1;
                     const int32_t cx = cT[b];
@@ -649,7 +663,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
                     cur = b + 1;
                 }
-                if (cur >= kTile) break;
+                if (cur >= kTile) return false;
                 // exit: first of SL/TP (intrabar, from entry + 1; SL wins a same-bar tie), the
                 // signal exit and the forced exit at B-1 (SL/TP beat both on the same bar)
                 const bool lg = a.pos > 0;
@@ -659,7 +673,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 sltp_search(LO, cur, XL, XHm1, xlo, xhi);
                 const int xs = min(xlo, xhi);
                 const bool hit = xs < kTile && xs <= x;
-                if (!hit && x >= kTile) break;
+                if (!hit && x >= kTile) return false;
                 // one path for both exit kinds (no divergence): the trade's closes up to the bar
                 // before an SL/TP fill or up to a signal exit's bar, then the fill price (for a
                 // signal exit that is the last close again, which leaves the aggregate unchanged)
@@ -667,13 +681,20 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const int qi = hit ? x - 1 : x;  // >= a.sb - 1 (exits come after the entry bar)
                 const int32_t px = hit ? ((xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1) : cT[x];
                 const Agg seg = dst_query_bf(D, a.sb, max(qi, a.sb));
-                const Agg st = agg_merge(agg_merge(a.agg, qi < a.sb ? kAggId : seg), agg_one(px));
+                const Agg sp = qi < a.sb ? kAggId : seg;
+                const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
                 acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
                 a.ps1 += lg ? qx : (uint64_t)0 - qx;
                 a.ps2 += q2x;
                 a.pos = 0;
                 cur = x + 1;
+                return true;
+            };
+            if (trade(std::true_type{})) {
+#pragma unroll 1
+                while (trade(std::false_type{})) {
+                }
             }
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
