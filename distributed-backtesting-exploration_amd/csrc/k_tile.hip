@@ -680,8 +680,10 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 if (hit) x = xs;
                 const int qi = hit ? x - 1 : x;  // >= a.sb - 1 (exits come after the entry bar)
                 const int32_t px = hit ? ((xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1) : cT[x];
-                const Agg seg = dst_query_bf(D, a.sb, max(qi, a.sb));
-                const Agg sp = qi < a.sb ? kAggId : seg;
+                // qi < a.sb only for a fill at the first bar of the tile of a carried position;
+                // a trade opened in this tile exits after its entry bar a.sb, so qi >= a.sb
+                const Agg seg = dst_query_bf(D, a.sb, FIRST ? max(qi, a.sb) : qi);
+                const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
                 const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
                 acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
