@@ -1,0 +1,91 @@
+"""Trades at 64-bar tile edges: the walks peel the first trade of every tile (only it can start
+with a position carried in from earlier tiles; later trades of the tile open inside it), so the
+parity cases must hold both shapes often:
+
+* a carried Bollinger position filled by SL/TP on the FIRST bar of a tile (the one fill whose
+  path before the fill bar is empty in this tile: `k_tile.hip` boll walk, `qi < a.sb`);
+* a carried position closed in a tile and further trades (or reversals) after it in the same
+  tile (the non-first, merge-free walk iterations).
+
+The CPU test checks that the seeded cases below contain both shapes (oracle trade lists); the GPU
+test checks every field and trade of them bit-exact against the C oracle (oracle/oracle.c
+orc_boll / orc_ema_ols / orc_sma, docs/oracle_spec.md §4).
+"""
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from helpers import compare_summary, compare_trades, oracle_row
+
+CAP = 8192
+T = 64
+
+
+def _case(seed):
+    rng = np.random.default_rng(7000 + seed)
+    n = 3000 + int(rng.integers(0, 64))
+    c = 1_000_000 + np.cumsum(rng.integers(-6000, 6001, n))
+    c = np.clip(c, 10_000, 2**31 - 1).astype(np.int32)
+    hi = np.clip(c + rng.integers(0, 9000, n), 1, 2**31 - 1).astype(np.int32)
+    lo = np.clip(c - rng.integers(0, 9000, n), 1, 2**31 - 1).astype(np.int32)
+    return c, hi, lo
+
+
+GRIDS = {
+    "boll": lambda: D.Grid.boll([4, 9, 30], [1, 2, 4], [5, 25], [5, 40], k_den=2),
+    "ema_ols": lambda: D.Grid.ema_ols([3, 8, 40], [4, 16], band_bps=0),
+    "sma": lambda: D.Grid.sma([2, 3, 7], [4, 11, 50]),
+}
+ANN = {"boll": 98280, "ema_ols": 98280, "sma": 252}
+
+
+def _shapes(trades, n, close):
+    """(carried positions filled by SL/TP on a tile's first bar, tiles where a carried position
+    closes and another trade then opens in the same tile)."""
+    edge_fill = carried_then_more = 0
+    tr = [(int(t["entry_bar"]), int(t["exit_bar"]), int(t["exit_px"])) for t in trades[:n]]
+    for i, (e, x, px) in enumerate(tr):
+        carried = e // T < x // T
+        if carried and x % T == 0 and px != int(close[x]):
+            edge_fill += 1
+        if carried and i + 1 < len(tr) and tr[i + 1][0] // T == x // T:
+            carried_then_more += 1
+    return edge_fill, carried_then_more
+
+
+@pytest.mark.parametrize("strategy", ["boll", "ema_ols", "sma"])
+def test_cases_hold_tile_edge_shapes(strategy):
+    grid = GRIDS[strategy]()
+    edge = more = 0
+    for seed in range(2):
+        c, hi, lo = _case(seed)
+        orc, otr = oracle_row(strategy, grid, (c, hi, lo, c), ANN[strategy], CAP)
+        for p in range(grid.n_params):
+            assert int(orc[p]["n_trades"]) <= CAP
+            a, b = _shapes(otr[p], int(orc[p]["n_trades"]), c)
+            edge += a
+            more += b
+    if strategy == "boll":
+        assert edge >= 5, f"only {edge} SL/TP fills on a tile's first bar"
+    assert more >= 20, f"only {more} tiles with a carried close followed by another trade"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["boll", "ema_ols", "sma"])
+def test_tile_edge_trades_gpu(strategy):
+    grid = GRIDS[strategy]()
+    cases = [_case(seed) for seed in range(2)]
+    closes = [x[0] for x in cases]
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        if strategy == "sma":
+            e.load_ohlc(closes)
+        else:
+            e.load_ohlc(closes, [x[1] for x in cases], [x[2] for x in cases])
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, (c, hi, lo) in enumerate(cases):
+        orc, otr = oracle_row(strategy, grid, (c, hi, lo, c), ANN[strategy], CAP)
+        for p in range(grid.n_params):
+            where = f"{strategy} case {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
