@@ -778,9 +778,10 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 1);
     const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
     // at most one block per CU (config 4 on 8 GPUs: 250 symbols) leaves wave slots free: four
-    // task-only waves instead of two (8.37 -> 8.03 ms); with two blocks per CU four no longer fit
+    // task-only waves (8.17 -> 7.90 ms vs two); otherwise as many as keep the block at 8 waves,
+    // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms)
     const bool sparse = (long long)grid.x * grid.y <= device_cus();
-    const int xw = tile_extra_waves(pw + 1, sparse ? 4 : 2);
+    const int xw = tile_extra_waves(pw + 1, sparse ? 4 : std::max(2, std::min(3, 8 - (pw + 1))));
     const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
     if (g.ablate & 64)
