@@ -23,6 +23,7 @@
 //            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
 //            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 
@@ -641,7 +642,8 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     if (g.ablate & 128) lds = std::max(lds, (size_t)(g.ablate & 256 ? 80 : 60) * 1024);  // occupancy probe
     // blocks of more than 8 waves (config 5: one 16-wave block per CU) hide little LDS latency:
     // their reversal loop issues all of an iteration's reads before one wait
-    const bool one_trip = sh.block > 512;
+    bool one_trip = sh.block > 512;
+    if (const char* v = getenv("BT_ONE_TRIP")) one_trip = atoi(v) != 0;  // tuning aid
     if (g.ablate & 64)
         hipLaunchKernelGGL((sma_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity && one_trip)
