@@ -145,8 +145,6 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             if (!(err = copy_axis(1, c.slow, c.n_slow, "slow", 1, kMaxBars)).empty()) return err;
             const int64_t mf = *std::max_element(e->ax[0].begin(), e->ax[0].end());
             const int64_t ms = *std::max_element(e->ax[1].begin(), e->ax[1].end());
-            // exact key comparison needs fast*slow < 2^21 (see k_sma.hip)
-            if (mf * ms >= (1LL << 21)) return "SMA grid outside the exact-key range (max fast*slow >= 2^21)";
             e->grid.na = c.n_fast;
             e->grid.nb = c.n_slow;
             e->grid.nc = e->grid.nd = 1;
@@ -175,7 +173,6 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
         case BT_BOLL: {
             if (!(err = copy_axis(0, c.bwin, c.n_bwin, "bwin", 1, 1 << 16)).empty()) return err;
             if (!(err = copy_axis(1, c.k_num, c.n_k, "k_num", 0, 1 << 20)).empty()) return err;
-            if (c.n_k > 8) return "Bollinger grid: at most 8 k values";
             if (!(err = copy_axis(2, c.sl_bps, c.n_sl, "sl_bps", 0, 9999)).empty()) return err;
             if (!(err = copy_axis(3, c.tp_bps, c.n_tp, "tp_bps", 0, 9999)).empty()) return err;
             if (c.k_den < 1 || c.k_den > (1 << 20)) return "k_den out of range";
@@ -294,7 +291,7 @@ void run_impl(bt_engine* e) {
     out.n_trades = e->d_ntr[b].p;
     HIPCHK(hipMemsetAsync(e->d_ntr[b].p, 0, sizeof(unsigned long long), e->stream));
     out.dbg = nullptr;
-    if (e->grid.ablate & 64) {  // profiling stamps
+    if (BT_ABL(e->grid, 64)) {  // profiling stamps (profiling build only)
         e->d_dbg.ensure(32);
         HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, 32 * sizeof(unsigned long long), e->stream));
         out.dbg = e->d_dbg.p;
@@ -483,7 +480,9 @@ bt_engine* bt_engine_create(const bt_config* cfg, char* err, size_t errlen) {
         HIPCHK(hipEventCreateWithFlags(&e->ev_kdone, hipEventDisableTiming));
         for (int b = 0; b < 2; ++b) HIPCHK(hipEventCreateWithFlags(&e->ev_tdone[b], hipEventDisableTiming));
         upload_grid(e);
-        if (const char* ab = getenv("BT_ABLATE")) e->grid.ablate = atoi(ab);  // profiling aid
+#ifdef BT_PROFILING
+        if (const char* ab = getenv("BT_ABLATE")) e->grid.ablate = atoi(ab);  // profiling build only
+#endif
         return e;
     } catch (const HipFail& f) {
         delete e;

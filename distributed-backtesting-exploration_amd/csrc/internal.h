@@ -5,6 +5,15 @@
 
 #include "../../include/bt.h"
 
+// Profiling switches (phase ablation, s_memtime stamps, launch-shape overrides from the
+// environment) exist only in the profiling build (`make PROFILING=1` -> libbt_prof.so). In the
+// release libbt.so BT_ABL is the constant false: no environment variable can change a result.
+#ifdef BT_PROFILING
+#define BT_ABL(g, bit) (((g).ablate & (bit)) != 0)
+#else
+#define BT_ABL(g, bit) false
+#endif
+
 namespace bt {
 
 constexpr int kTile = 64;          // bars per LDS tile (one bit per bar in a 64-bit word)
@@ -27,7 +36,8 @@ struct Grid {
     int32_t ring;                  // prefix ring length >= wmax + 3 kTile (SMA: a power of two;
                                    // tile kernels: a multiple of kTile)
     double sqrt_ann;               // sqrt((double)annualization), computed on the host
-    int32_t ablate;                // profiling only (env BT_ABLATE): phases to skip, 0 = none
+    int32_t ablate;                // BT_PROFILING builds only (env BT_ABLATE): phases to skip;
+                                   // always 0 in the release library (read through BT_ABL)
     const int32_t* a;              // device arrays
     const int32_t* b;
     const int32_t* c;

@@ -18,7 +18,7 @@
 //            unsigned min that detects equal keys; without equal keys G (fast > slow) = ~L.
 //            Keys are monotone in the exact SMA, so a strict key order is the exact order; equal
 //            keys (rare: ~1e-4 of lane-tiles on config 2) are settled exactly (F*s vs L*f in
-//            f64, products < 2^53). The whole tile's position path then follows
+//            int64, products < 2^59). The whole tile's position path then follows
 //            bit-parallel: a set/reset latch is an add-with-carry (LONG = carries of
 //            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
 //            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     const bool helper = (tid >> 6) == nwaves - 1;
     // the wave before it builds the drawdown tables (stage_dst); profiling bit 16 keeps both
     // parts of stage 1 on the last wave
-    const bool split = !(g.ablate & 16);
+    const bool split = !BT_ABL(g, 16);
     const bool dstw = split && (tid >> 6) == nwaves - 2;
     const bool dsth = helper && !split;
     const int nparam_threads = dedicated ? (int)blockDim.x - 64 : (int)blockDim.x;
@@ -456,9 +456,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         const int t0 = k * kTile;
         // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
         // (tile k+1) on every wave, balanced dynamically
-        if ((helper || dstw) && k + 2 < ntiles && !(g.ablate & 1)) {
+        if ((helper || dstw) && k + 2 < ntiles && !BT_ABL(g, 1)) {
             // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
-            if (!(g.ablate & 32)) __builtin_amdgcn_s_setprio(2);
+            if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
             const int s = (k + 2) % kStages;
             if (helper)
                 stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
             const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
             uint32_t l0 = 0, l1 = 0, z = ~0u;
-            if (!(g.ablate & 4)) {
+            if (!BT_ABL(g, 4)) {
                 // all reads at immediate offsets from one address per row
 #pragma unroll
                 for (int v = 0; v < 16; ++v) {
@@ -519,9 +519,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                     const int b = __builtin_ctzll(T);
                     T &= T - 1;
                     const int t = t0 + b;
+                    // window sums are exact in the ring (< 2^53) and < 2^31 w; F s and L f
+                    // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
+                    // so the tie is settled in int64 for every grid the engine accepts
                     const double top = ring[(t + 1) & (R - 1)];
-                    const double Fs = (top - ring[(t + 1 - fw) & (R - 1)]) * (double)sw;
-                    const double Lf = (top - ring[(t + 1 - sw) & (R - 1)]) * (double)fw;
+                    const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
+                    const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
                     G |= (uint64_t)(Fs > Lf) << b;
                     L |= (uint64_t)(Fs < Lf) << b;
                 }
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             }
             BT_STAMP(3)
             uint64_t Fw = F;
-            if (g.ablate & 8) {  // profiling: drop the trade events (keep F live)
+            if (BT_ABL(g, 8)) {  // profiling: drop the trade events (keep F live)
                 asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
                 Fw = 0;
             }
@@ -579,7 +582,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             BT_STAMP(5)
             if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !(g.ablate & 2))
+        if (k + 1 < ntiles && !BT_ABL(g, 2))
             stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
                        ctr, (uint32_t)(k + 1), nwaves, lane);
         BT_STAMP(1)
@@ -639,14 +642,18 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     const SmaShape sh = sma_shape(g.n_params);
     const dim3 grid(n_sym, sh.gy), block(sh.block);
     size_t lds = sma_lds_bytes(g);
-    if (g.ablate & 128) lds = std::max(lds, (size_t)(g.ablate & 256 ? 80 : 60) * 1024);  // occupancy probe
     // blocks of more than 8 waves (config 5: one 16-wave block per CU) hide little LDS latency:
     // their reversal loop issues all of an iteration's reads before one wait
     bool one_trip = sh.block > 512;
+#ifdef BT_PROFILING
+    if (BT_ABL(g, 128)) lds = std::max(lds, (size_t)(g.ablate & 256 ? 80 : 60) * 1024);  // occupancy probe
     if (const char* v = getenv("BT_ONE_TRIP")) one_trip = atoi(v) != 0;  // tuning aid
-    if (g.ablate & 64)
+    if (BT_ABL(g, 64)) {
         hipLaunchKernelGGL((sma_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
-    else if (parity && one_trip)
+        return hipGetLastError();
+    }
+#endif
+    if (parity && one_trip)
         hipLaunchKernelGGL((sma_kernel<true, false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity)
         hipLaunchKernelGGL((sma_kernel<true, false, false>), grid, block, lds, st, syms, close, g, out, sh.dedicated);

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         double* E = ebuf + (T & 1) * estage + lane * kEStride;
         // the chain is the block's per-tile critical path (three dependent fp64 operations per
         // bar): issue it ahead of the other waves on its SIMD
-        if (!(g.ablate & 32)) __builtin_amdgcn_s_setprio(3);
+        if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(3);
         if (lane < nsp) {
             if (t1 > 0 && t1 + kTile <= B) {
 #pragma unroll
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             cpre = ldc(crow, B, t0 + 3 * kTile + lane, 0);
         }
         if (STAMPS) sa.mark(0);
-        if (active && !(g.ablate & 8)) {
+        if (active && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !(g.ablate & 2)) flags(k + 1);
+        if (k + 1 < ntiles && !BT_ABL(g, 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 //           from an LDS counter (z tests in fp64 with an exact int128 fallback);
 //   parameter waves, tile k: one trade per loop iteration (entry at the first z signal, exit at
 //           the first of SL/TP / signal / forced), O(1) accounting per trade.
-constexpr int kMaxK = 8;             // z thresholds per window (engine-validated)
+constexpr int kMaxK = 8;             // z thresholds tested per unrolled pass of a window task
 
 // 8-bit mask of v_j > X over a (4+4)-int32 group, bit j = element j: the sign bit of X - v_j
 // (no overflow: prices, padding and levels all lie in [0, 2^31)) shifted in by v_alignbit,
@@ -558,8 +558,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const double lh = (Dd * Dd) * kd2d;
             // Q < 2^87: (Q >> 32) < 2^55 rounds once, the low word adds one more rounding
             const double Qd = (double)(int64_t)(Q >> 32) * 0x1p32 + (double)(uint32_t)Q;
+#pragma unroll 1
+            for (int q0 = 0; q0 < nk; q0 += kMaxK) {  // one pass for grids of <= 8 k values
 #pragma unroll
-            for (int q = 0; q < kMaxK; ++q) {
+            for (int qq = 0; qq < kMaxK; ++qq) {
+                const int q = q0 + qq;
                 if (q >= nk) break;
                 const double rh = kn2d[q] * Qd;
                 // lh and rh are within 2^-50 relative of the exact sides: outside a 2^-48 band
@@ -576,6 +579,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     Wd[2 * ((int)o * nk + q)] = zl;
                     Wd[2 * ((int)o * nk + q) + 1] = zh;
                 }
+            }
             }
             const uint64_t dp = __ballot(valid && Dv >= 0), dn = __ballot(valid && Dv <= 0);
             if (lane == 0) {
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             lpre = ldc(lrow, B, tn, INT32_MAX);
         }
         if (STAMPS) sa.mark(0);
-        if (active && !(g.ablate & 8)) {
+        if (active && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
@@ -702,7 +706,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !(g.ablate & 2)) flags(k + 1);
+        if (k + 1 < ntiles && !BT_ABL(g, 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
@@ -722,13 +726,17 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 // 12.3 -> 12.0 ms (250 symbols: 9.95 -> 9.76 ms); four no longer fit two blocks (19.4 ms).
 static int tile_param_waves(int need, int cap) {
     int pw = std::min(need, cap);
+#ifdef BT_PROFILING
     if (const char* v = getenv("BT_PW")) pw = std::max(1, std::min(atoi(v), pw));  // tuning aid
+#endif
     return pw;
 }
 
 static int tile_lanes_per_wave() {
     int l = 64;
+#ifdef BT_PROFILING
     if (const char* v = getenv("BT_LPW")) l = std::max(1, std::min(atoi(v), 64));  // tuning aid
+#endif
     return l;
 }
 
@@ -745,7 +753,9 @@ static int device_cus() {
 }
 
 static int tile_extra_waves(int used, int x) {
+#ifdef BT_PROFILING
     if (const char* v = getenv("BT_XW")) x = atoi(v);  // tuning aid
+#endif
     return std::max(0, std::min(x, 16 - used));
 }
 
@@ -761,9 +771,13 @@ hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* clo
     const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
     const dim3 block(64 * (pw + 2 + xw));
     const size_t lds = ema_lds_bytes(g);
-    if (g.ablate & 64)
+#ifdef BT_PROFILING
+    if (BT_ABL(g, 64)) {
         hipLaunchKernelGGL((ema_tile_kernel<false, true>), grid, block, lds, st, syms, close, g, out, xw, lpw);
-    else if (parity)
+        return hipGetLastError();
+    }
+#endif
+    if (parity)
         hipLaunchKernelGGL((ema_tile_kernel<true, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
     else
         hipLaunchKernelGGL((ema_tile_kernel<false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
@@ -784,9 +798,13 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     const int xw = tile_extra_waves(pw + 1, sparse ? 4 : std::max(2, std::min(3, 8 - (pw + 1))));
     const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
-    if (g.ablate & 64)
+#ifdef BT_PROFILING
+    if (BT_ABL(g, 64)) {
         hipLaunchKernelGGL((boll_tile_kernel<false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
-    else if (parity)
+        return hipGetLastError();
+    }
+#endif
+    if (parity)
         hipLaunchKernelGGL((boll_tile_kernel<true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
     else
         hipLaunchKernelGGL((boll_tile_kernel<false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);

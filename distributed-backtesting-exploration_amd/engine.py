@@ -221,7 +221,7 @@ def config4_grid():
 
 
 def config5_grid():
-    # SMA fast 32 x slow 32 on 1-min bars; max fast*slow = 160*6400 < 2^21 (exact keys)
+    # SMA fast 32 x slow 32 on 1-min bars
     return Grid.sma(range(5, 161, 5), range(200, 6401, 200), annualization=98280)
 
 

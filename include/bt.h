@@ -39,7 +39,10 @@ enum bt_flags {
 enum bt_freq { BT_DAILY = 0, BT_MINUTE = 1 };
 
 /* Engine configuration. The proto carries no strategy or params (proto:13-16), so the grid is
- * worker-side configuration (SURVEY.md §7 hard part 5). Arrays are copied at create time. */
+ * worker-side configuration (SURVEY.md §7 hard part 5). Arrays are copied at create time.
+ * Accepted domain (docs/oracle_spec.md §7): windows up to 4,096 bars always, longer ones while the
+ * prefix ring fits 160 KB of LDS; EMA at most 64 spans; Bollinger w * max(k_num, k_den) < 2^32;
+ * at most 2^20 params. Anything else is refused by bt_engine_create, never approximated. */
 typedef struct bt_config {
     int32_t strategy;                 /* enum bt_strategy */
     /* SMA crossover: params = n_fast x n_slow, param = i_fast * n_slow + i_slow */
@@ -164,8 +167,9 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n);
 /* Average device time of the dominant kernel (BT_FLAG_TIMING), and how many launches. */
 int32_t bt_kernel_timing(bt_engine* e, double* total_ms, int64_t* launches, const char** name);
 int32_t bt_reset_timing(bt_engine* e);
-/* Profiling aid: per-phase s_memtime sums of the last run when the engine was created with
- * BT_ABLATE=64 in the environment (developer use; n <= 32). */
+/* Profiling aid of the developer build libbt_prof.so only (`make PROFILING=1`, env BT_ABLATE=64):
+ * per-phase s_memtime sums of the last run (n <= 32). The release libbt.so reads no environment
+ * variable and always returns -1 ("no debug stamps") here. */
 int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n);
 
 /* ---- top-k merge (host): merge sorted record lists from several shards (RCCL gather). */

@@ -333,3 +333,61 @@ def test_pipelined_topk_fetch():
         for slot, (top, trades) in enumerate(refs):
             got, n = e.topk_fetch_wait(slot)
             assert got.tolist() == top.tolist() and n == trades
+
+
+@pytest.mark.parametrize("hi_prices", [False, True])
+def test_sma_large_window_products(hi_prices):
+    """SMA grids whose window products f*s pass 2^53 (600 x 4096, 4096 x 4000): equal floor keys
+    are settled with F*s vs L*f in int64 (k_sma.hip), so every grid the LDS ring holds is exact.
+    hi_prices: prices just below 2^31 with 0-3 tick noise, where keys tie on most bars and the
+    products (~2^55) are beyond fp64's exact range."""
+    grid = D.Grid.sma([600, 4096, 37], [4096, 4000, 5000], annualization=98280)
+    bars = 9000
+    if hi_prices:
+        rng = np.random.default_rng(4)
+        closes = [(2**31 - 2**20 - 1 - rng.integers(0, 4, bars)).astype(np.int32) for _ in range(2)]
+    else:
+        closes = [F.gen(0x5EED, s, bars, 1)[3] for s in (3, 4)]
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_ohlc(closes)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("sma", grid, (cl, cl, cl, cl), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"large windows hi={hi_prices} sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_release_library_ignores_ablate_env(monkeypatch):
+    """BT_ABLATE in the environment (a profiling switch of libbt_prof.so) must not change a
+    release-library result: bit-identical summaries with and without it."""
+    grid = D.Grid.boll([10, 45], [3, 5], [50], [100, 400], k_den=2)
+    res = []
+    for env in (None, "15"):
+        if env:
+            monkeypatch.setenv("BT_ABLATE", env)
+        with D.Engine(grid) as e:
+            e.load_synthetic(0x5EED, 0, 4, 3000, D.BT_MINUTE)
+            e.run()
+            res.append(e.summaries().copy())
+    assert res[0].tobytes() == res[1].tobytes() and int(res[0]["n_trades"].sum()) > 0
+
+
+def test_boll_many_k_values():
+    """Bollinger grids with more than 8 z thresholds per window (condition words in passes of
+    8 k values, k_tile.hip): 12 k values x 3 windows, bit-exact trades vs the oracle."""
+    grid = D.Grid.boll([5, 20, 90], list(range(1, 13)), [50], [100], k_den=4)
+    bars = 4000
+    o, h, lo, c = _gen(0x5EED, [21, 22], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 21, 2, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(2):
+        orc, otr = oracle_row("boll", grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"boll 12 k sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
