@@ -20,6 +20,12 @@ bool parse_csv(const uint8_t* buf, size_t len, Bars& out, std::string& err);
 bool is_binary_payload(const uint8_t* buf, size_t len);
 size_t binary_payload_size(int32_t n, bool volume);
 bool parse_binary(const uint8_t* buf, size_t len, Bars& out, std::string& err);
+// Header check only (magic, bar count, flags, exact length): the batch ingest sizes its rows
+// from it before decoding.
+bool binary_header(const uint8_t* buf, size_t len, int32_t& n_bars, std::string& err);
+// Validate and copy the high/low/close columns (h, l may be null) in one pass.
+bool decode_binary_into(const uint8_t* buf, size_t len, int32_t* h, int32_t* l, int32_t* c,
+                        std::string& err);
 // Job.File in either format (CSV or binary columns), dispatched on the magic.
 bool parse_job(const uint8_t* buf, size_t len, Bars& out, std::string& err);
 size_t encode_binary(const int32_t* o, const int32_t* h, const int32_t* l, const int32_t* c,

@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <charconv>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -111,6 +113,15 @@ struct bt_engine {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_pool;
     double kernel_ms = 0.0;
     int64_t launches = 0;
+    // bt_run_batch: pinned host staging of the columns in device row layout (c, h, l), the
+    // batch's summaries read back in one copy, phase events and the last batch's profile
+    int32_t* h_stage[3] = {nullptr, nullptr, nullptr};
+    size_t stage_rows[3] = {0, 0, 0};
+    bt_summary* h_sum = nullptr;
+    size_t h_sum_n = 0;
+    hipEvent_t ev_batch[4] = {nullptr, nullptr, nullptr, nullptr};
+    bt_batch_profile prof{};
+    int64_t n_errors = 0;
 };
 
 namespace {
@@ -215,28 +226,48 @@ void upload_grid(bt_engine* e) {
     }
 }
 
-// Lay out rows (64-element aligned) and allocate the columns the strategy needs.
-void layout(bt_engine* e, int32_t n_sym, const int32_t* bars, const int64_t* ids) {
-    e->syms.resize(n_sym);
-    int64_t off = 0;
-    for (int32_t s = 0; s < n_sym; ++s) {
-        e->syms[s].off = off;
-        e->syms[s].bars = bars[s];
-        e->syms[s].id = (int32_t)ids[s];
-        off += ((int64_t)bars[s] + kRowAlign - 1) / kRowAlign * kRowAlign;
-    }
-    e->rows = off;
+int64_t align_rows(int64_t bars) { return (bars + kRowAlign - 1) / kRowAlign * kRowAlign; }
+
+// Install a dataset: symbol descriptors (row offsets into the columns) and `rows` rows per
+// column; allocates the columns the strategy needs.
+void set_dataset(bt_engine* e, std::vector<SymDesc>&& syms, int64_t rows) {
+    e->syms = std::move(syms);
+    e->rows = rows;
+    const size_t n_sym = e->syms.size();
     e->d_syms.ensure(std::max<size_t>(1, n_sym));
     if (n_sym)
         HIPCHK(hipMemcpyAsync(e->d_syms.p, e->syms.data(), n_sym * sizeof(SymDesc),
                               hipMemcpyHostToDevice, e->stream));
-    const size_t rows = std::max<int64_t>(1, off);
-    e->d_c.ensure(rows);
+    const size_t r = std::max<int64_t>(1, rows);
+    e->d_c.ensure(r);
     if (has_hl(e)) {
-        e->d_h.ensure(rows);
-        e->d_l.ensure(rows);
+        e->d_h.ensure(r);
+        e->d_l.ensure(r);
     }
     e->ran = false;
+}
+
+// Lay out rows (64-element aligned) and allocate the columns the strategy needs.
+void layout(bt_engine* e, int32_t n_sym, const int32_t* bars, const int64_t* ids) {
+    std::vector<SymDesc> syms((size_t)n_sym);
+    int64_t off = 0;
+    for (int32_t s = 0; s < n_sym; ++s) {
+        syms[s].off = off;
+        syms[s].bars = bars[s];
+        syms[s].id = (int32_t)ids[s];
+        off += align_rows(bars[s]);
+    }
+    set_dataset(e, std::move(syms), off);
+}
+
+template <class T>
+void ensure_pinned(T*& p, size_t& have, size_t want) {
+    if (want <= have && p) return;
+    if (p) HIPCHK(hipHostFree(p));
+    p = nullptr;
+    have = 0;
+    HIPCHK(hipHostMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)));
+    have = std::max<size_t>(want, 1);
 }
 
 TopkWork topk_work(bt_engine* e) {
@@ -385,20 +416,39 @@ std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     return res;
 }
 
-std::string fmt_job(const bt_summary* r, int32_t P) {
-    std::string s;
-    s.reserve((size_t)P * 110);
-    char line[256];
-    for (int32_t p = 0; p < P; ++p) {
-        const bt_summary& x = r[p];
-        int n = snprintf(line, sizeof line,
-                         "{\"param\":%d,\"n\":%d,\"pnl\":%lld,\"mdd\":%lld,\"exp\":%lld,"
-                         "\"sharpe\":\"%.17g\",\"h\":\"%016llx\"}\n",
-                         p, x.n_trades, (long long)x.pnl, (long long)x.mdd,
-                         (long long)x.exposure, x.sharpe, (unsigned long long)x.hash);
-        s.append(line, (size_t)n);
-    }
-    return s;
+// One CompleteRequest.data line (spec §6). std::to_chars gives printf's "%.17g" (general
+// format, precision 17) and plain decimal integers without the locale and format-string work of
+// snprintf; tests/test_abi_cpu.py checks the bytes against Python's "%.17g" / "%016x".
+char* put_lit(char* q, const char* s) {
+    while (*s) *q++ = *s++;
+    return q;
+}
+
+char* fmt_line(char* q, int32_t p, const bt_summary& x) {
+    static const char kHex[] = "0123456789abcdef";
+    q = put_lit(q, "{\"param\":");
+    q = std::to_chars(q, q + 16, p).ptr;
+    q = put_lit(q, ",\"n\":");
+    q = std::to_chars(q, q + 16, x.n_trades).ptr;
+    q = put_lit(q, ",\"pnl\":");
+    q = std::to_chars(q, q + 24, (long long)x.pnl).ptr;
+    q = put_lit(q, ",\"mdd\":");
+    q = std::to_chars(q, q + 24, (long long)x.mdd).ptr;
+    q = put_lit(q, ",\"exp\":");
+    q = std::to_chars(q, q + 24, (long long)x.exposure).ptr;
+    q = put_lit(q, ",\"sharpe\":\"");
+    q = std::to_chars(q, q + 32, x.sharpe, std::chars_format::general, 17).ptr;
+    q = put_lit(q, "\",\"h\":\"");
+    for (int i = 15; i >= 0; --i) *q++ = kHex[(x.hash >> (4 * i)) & 15];
+    return put_lit(q, "\"}\n");
+}
+
+constexpr size_t kLineMax = 192;  // longest line: 10 + 11 + 20 x 3 + 24 + 16 + fixed text < 192
+
+size_t fmt_job_into(const bt_summary* r, int32_t P, char* out) {
+    char* q = out;
+    for (int32_t p = 0; p < P; ++p) q = fmt_line(q, p, r[p]);
+    return (size_t)(q - out);
 }
 
 std::string json_escape(const std::string& in) {
@@ -422,6 +472,183 @@ char* dup_string(const std::string& s) {
     memcpy(p, s.data(), s.size());
     p[s.size()] = 0;
     return p;
+}
+
+
+// Host threads of the batch ingest: host_threads, else the machine's, at most 16 (the worker's
+// share of a GPU box; /root/reference/src/worker/handlers.rs:35 reports num_cpus/2 as cores).
+int host_threads(const bt_engine* e, size_t n) {
+    int nt = e->cfg.host_threads > 0
+                 ? e->cfg.host_threads
+                 : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    return (int)std::min<size_t>((size_t)nt, std::max<size_t>(1, n));
+}
+
+// f(i) for i in [0, n) on nt threads (f must not throw).
+template <class F>
+void parallel_for(int nt, size_t n, const F& f) {
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    };
+    if (nt <= 1 || n <= 1) {
+        work();
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt);
+    for (int i = 0; i < nt; ++i) th.emplace_back(work);
+    for (auto& t : th) t.join();
+}
+
+struct JobSlot {
+    bool ok = false, binary = false;
+    int32_t bars = 0;
+    int64_t row = 0;
+    size_t sym = 0;
+    Bars parsed;  // CSV jobs only (binary payloads decode straight into the staging rows)
+    std::string err;
+};
+
+double ms_between(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+}
+
+// The JobsReply as one GPU batch (drop-in for process_incoming_job's loop,
+// /root/reference/src/worker/process.rs:21-25):
+//   1. per job (host threads): binary payloads -> bar count from the header; CSV -> parsed;
+//   2. rows of the good jobs laid out 64-aligned in pinned host staging;
+//   3. per job (host threads): binary payloads validated and decoded straight into their rows
+//      in one pass (decode_binary_into), CSV bars copied in;
+//   4. one async H2D per column, the strategy kernel, one D2H of every summary, one wait;
+//   5. per job (host threads): the CompleteRequest.data string.
+void run_batch_impl(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* outs) {
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    activate(e);
+    sync_all(e);  // staging and h_sum may still be in use by an earlier call
+    bt_batch_profile pr{};
+    pr.n_jobs = (int64_t)n;
+    const int nt = host_threads(e, n);
+    const bool hl = has_hl(e);
+    std::vector<JobSlot> js(n);
+    for (size_t i = 0; i < n; ++i) pr.payload_bytes += (int64_t)jobs[i].len;
+    parallel_for(nt, n, [&](size_t i) {
+        JobSlot& j = js[i];
+        try {
+            const uint8_t* buf = jobs[i].file;
+            const size_t len = jobs[i].len;
+            if (!buf && len) {
+                j.err = "null Job.File";
+            } else if (buf && is_binary_payload(buf, len)) {
+                j.binary = true;
+                j.ok = binary_header(buf, len, j.bars, j.err);
+            } else {
+                j.ok = parse_csv(buf, len, j.parsed, j.err);
+                j.bars = (int32_t)j.parsed.c.size();
+            }
+        } catch (...) {
+            j.ok = false;
+            j.err = "parse failure";
+        }
+    });
+    int64_t rows = 0;
+    for (JobSlot& j : js)
+        if (j.ok) {
+            j.row = rows;
+            rows += align_rows(j.bars);
+        }
+    const int ncol = hl ? 3 : 1;
+    for (int k = 0; k < ncol; ++k) ensure_pinned(e->h_stage[k], e->stage_rows[k], (size_t)std::max<int64_t>(rows, 1));
+    parallel_for(nt, n, [&](size_t i) {
+        JobSlot& j = js[i];
+        if (!j.ok) return;
+        try {
+            int32_t* c = e->h_stage[0] + j.row;
+            int32_t* h = hl ? e->h_stage[1] + j.row : nullptr;
+            int32_t* l = hl ? e->h_stage[2] + j.row : nullptr;
+            if (j.binary) {
+                j.ok = decode_binary_into(jobs[i].file, jobs[i].len, h, l, c, j.err);
+            } else {
+                memcpy(c, j.parsed.c.data(), (size_t)j.bars * 4);
+                if (hl) {
+                    memcpy(h, j.parsed.h.data(), (size_t)j.bars * 4);
+                    memcpy(l, j.parsed.l.data(), (size_t)j.bars * 4);
+                }
+                j.parsed = Bars();  // release early
+            }
+        } catch (...) {
+            j.ok = false;
+            j.err = "ingest failure";
+        }
+    });
+    // a job that failed in step 3 leaves its rows unreferenced
+    std::vector<SymDesc> syms;
+    e->n_errors = 0;
+    for (JobSlot& j : js) {
+        if (!j.ok) {
+            ++e->n_errors;
+            continue;
+        }
+        j.sym = syms.size();
+        syms.push_back(SymDesc{j.row, j.bars, (int32_t)syms.size()});
+        pr.bars += j.bars;
+    }
+    const auto t_staged = clk::now();
+    pr.host_ingest_ms = ms_between(t_start, t_staged);
+    pr.n_failed = e->n_errors;
+    const int32_t P = e->P;
+    const size_t nres = syms.size() * (size_t)P;
+    if (!syms.empty()) {
+        for (hipEvent_t& ev : e->ev_batch)
+            if (!ev) HIPCHK(hipEventCreate(&ev));
+        ensure_pinned(e->h_sum, e->h_sum_n, nres);
+        set_dataset(e, std::move(syms), rows);
+        HIPCHK(hipEventRecord(e->ev_batch[0], e->stream));
+        int32_t* dst[3] = {e->d_c.p, e->d_h.p, e->d_l.p};
+        for (int k = 0; k < ncol; ++k)
+            HIPCHK(hipMemcpyAsync(dst[k], e->h_stage[k], (size_t)rows * 4, hipMemcpyHostToDevice,
+                                  e->stream));
+        HIPCHK(hipEventRecord(e->ev_batch[1], e->stream));
+        run_impl(e);
+        HIPCHK(hipEventRecord(e->ev_batch[2], e->stream));
+        HIPCHK(hipMemcpyAsync(e->h_sum, e->d_sum[e->cur].p, nres * sizeof(bt_summary),
+                              hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipEventRecord(e->ev_batch[3], e->stream));
+        sync_all(e);
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev_batch[0], e->ev_batch[1]));
+        pr.upload_ms = ms;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev_batch[1], e->ev_batch[2]));
+        pr.compute_ms = ms;
+        HIPCHK(hipEventElapsedTime(&ms, e->ev_batch[2], e->ev_batch[3]));
+        pr.readback_ms = ms;
+    }
+    const auto t_dev = clk::now();
+    std::atomic<bool> alloc_fail{false};
+    parallel_for(nt, n, [&](size_t i) {
+        try {
+            const JobSlot& j = js[i];
+            if (j.ok) {
+                char* buf = (char*)malloc((size_t)P * kLineMax + 1);
+                if (!buf) throw std::bad_alloc();
+                const size_t len = fmt_job_into(e->h_sum + j.sym * (size_t)P, P, buf);
+                buf[len] = 0;
+                char* fit = (char*)realloc(buf, len + 1);
+                outs[i] = bt_job_out{fit ? fit : buf, len, 0, j.bars};
+            } else {
+                const std::string m = "{\"error\":\"" + json_escape(j.err) + "\"}\n";
+                outs[i] = bt_job_out{dup_string(m), m.size(), -1, 0};
+            }
+        } catch (...) {
+            alloc_fail = true;
+        }
+    });
+    if (alloc_fail) throw std::bad_alloc();
+    const auto t_end = clk::now();
+    pr.format_ms = ms_between(t_dev, t_end);
+    pr.total_ms = ms_between(t_start, t_end);
+    e->prof = pr;
 }
 
 #define ABI_GUARD(fail, ...)                                   \
@@ -541,6 +768,11 @@ void bt_engine_destroy(bt_engine* e) {
             e->slot_armed[i] = false;
         }
         e->topk_ready = false;
+        for (int i = 0; i < 3; ++i)
+            if (e->h_stage[i]) (void)hipHostFree(e->h_stage[i]);
+        if (e->h_sum) (void)hipHostFree(e->h_sum);
+        for (hipEvent_t& ev : e->ev_batch)
+            if (ev) (void)hipEventDestroy(ev);
         if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
         if (e->tstream) (void)hipStreamDestroy(e->tstream);
         e->tstream = nullptr;
@@ -579,22 +811,22 @@ int32_t bt_load_ohlc(bt_engine* e, int32_t n_sym, const int64_t* sym_ids, const 
         for (int32_t s = 0; s < n_sym; ++s)
             if (bars[s] < 1 || bars[s] > kMaxBars) throw HipFail{"bad bar count"};
         activate(e);
+        sync_all(e);  // the pinned staging may still feed an earlier upload
         layout(e, n_sym, bars, sym_ids);
-        // stage through one contiguous host buffer per column with the device row layout
-        std::vector<int32_t> tmp((size_t)std::max<int64_t>(1, e->rows));
-        auto put = [&](const int32_t* src, int32_t* dst) {
-            for (int32_t s = 0; s < n_sym; ++s)
-                memcpy(tmp.data() + e->syms[s].off, src + row_off[s], (size_t)bars[s] * 4);
-            HIPCHK(hipMemcpyAsync(dst, tmp.data(), (size_t)e->rows * 4, hipMemcpyHostToDevice,
-                                  e->stream));
-            sync_all(e);
-        };
+        // stage into pinned host rows with the device row layout, then one async copy per
+        // column and a single wait
+        const int ncol = has_hl(e) ? 3 : 1;
+        const int32_t* src[3] = {c, h, l};
+        int32_t* dst[3] = {e->d_c.p, e->d_h.p, e->d_l.p};
         if (e->rows > 0) {
-            put(c, e->d_c.p);
-            if (has_hl(e)) {
-                put(h, e->d_h.p);
-                put(l, e->d_l.p);
+            for (int k = 0; k < ncol; ++k) {
+                ensure_pinned(e->h_stage[k], e->stage_rows[k], (size_t)e->rows);
+                for (int32_t s = 0; s < n_sym; ++s)
+                    memcpy(e->h_stage[k] + e->syms[s].off, src[k] + row_off[s], (size_t)bars[s] * 4);
+                HIPCHK(hipMemcpyAsync(dst[k], e->h_stage[k], (size_t)e->rows * 4,
+                                      hipMemcpyHostToDevice, e->stream));
             }
+            sync_all(e);
         }
         return 0;
     })
@@ -716,6 +948,7 @@ int32_t bt_read_stats(bt_engine* e, bt_stats* out) {
         st.n_symbols = (int64_t)e->syms.size();
         st.n_params = e->P;
         for (const SymDesc& s : e->syms) st.bar_evals += (int64_t)s.bars * e->P;
+        st.errors = e->n_errors;
         if (e->ran) {
             unsigned long long n = 0;
             HIPCHK(hipMemcpy(&n, e->d_ntr[e->cur].p, sizeof n, hipMemcpyDeviceToHost));
@@ -775,86 +1008,31 @@ int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* 
     ABI_GUARD(-1, {
         if (!e || (n > 0 && (!jobs || !outs))) throw HipFail{"bad arguments"};
         for (size_t i = 0; i < n; ++i) outs[i] = bt_job_out{nullptr, 0, 0, 0};
-        // 1. parse every job (host threads; the worker's single compute thread calls us,
-        //    /root/reference/src/worker/main.rs:38-42)
-        std::vector<Bars> bars(n);
-        std::vector<std::string> errs(n);
-        std::vector<char> ok(n, 0);
-        int nt = e->cfg.host_threads > 0 ? e->cfg.host_threads
-                                         : (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-        nt = (int)std::min<size_t>((size_t)nt, std::max<size_t>(1, n));
-        std::atomic<size_t> next{0};
-        auto work = [&]() {
-            for (size_t i; (i = next.fetch_add(1)) < n;) {
-                try {
-                    ok[i] = parse_job(jobs[i].file, jobs[i].len, bars[i], errs[i]) ? 1 : 0;
-                } catch (...) {
-                    errs[i] = "parse failure";
-                    ok[i] = 0;
-                }
-            }
-        };
-        if (nt <= 1) {
-            work();
-        } else {
-            std::vector<std::thread> th;
-            for (int i = 0; i < nt; ++i) th.emplace_back(work);
-            for (auto& t : th) t.join();
-        }
-        // 2. one HBM-resident batch of the good jobs
-        std::vector<int64_t> ids, offs;
-        std::vector<int32_t> nb;
-        std::vector<size_t> job_of;
-        int64_t rows = 0;
-        for (size_t i = 0; i < n; ++i) {
-            if (!ok[i]) continue;
-            ids.push_back((int64_t)job_of.size());
-            offs.push_back(rows);
-            nb.push_back((int32_t)bars[i].c.size());
-            rows += (int64_t)bars[i].c.size();
-            job_of.push_back(i);
-        }
-        if (!job_of.empty()) {
-            std::vector<int32_t> C((size_t)rows), H, L;
-            if (has_hl(e)) {
-                H.resize((size_t)rows);
-                L.resize((size_t)rows);
-            }
-            for (size_t k = 0; k < job_of.size(); ++k) {
-                const Bars& b = bars[job_of[k]];
-                memcpy(C.data() + offs[k], b.c.data(), b.c.size() * 4);
-                if (has_hl(e)) {
-                    memcpy(H.data() + offs[k], b.h.data(), b.h.size() * 4);
-                    memcpy(L.data() + offs[k], b.l.data(), b.l.size() * 4);
-                }
-            }
-            if (bt_load_ohlc(e, (int32_t)job_of.size(), ids.data(), nb.data(), offs.data(),
-                             has_hl(e) ? H.data() : nullptr, has_hl(e) ? L.data() : nullptr,
-                             C.data()) != 0)
-                throw HipFail{g_err};
-            run_impl(e);
-            sync_all(e);
-        }
-        // 3. one CompleteRequest.data string per job, in job order
-        std::vector<bt_summary> res((size_t)e->P);
-        size_t k = 0;
-        for (size_t i = 0; i < n; ++i) {
-            std::string s;
-            if (ok[i]) {
-                HIPCHK(hipMemcpy(res.data(), e->d_sum[e->cur].p + k * (size_t)e->P,
-                                 (size_t)e->P * sizeof(bt_summary), hipMemcpyDeviceToHost));
-                s = fmt_job(res.data(), e->P);
-                outs[i].status = 0;
-                outs[i].n_bars = (int32_t)bars[i].c.size();
-                ++k;
-            } else {
-                s = "{\"error\":\"" + json_escape(errs[i]) + "\"}\n";
-                outs[i].status = -1;
-            }
-            outs[i].data = dup_string(s);
-            outs[i].len = s.size();
+        try {
+            run_batch_impl(e, n, jobs, outs);
+        } catch (...) {
+            bt_job_out_free(outs, n);  // a failed call leaves no string allocated
+            throw;
         }
         return 0;
+    })
+}
+
+int32_t bt_last_batch_profile(bt_engine* e, bt_batch_profile* out) {
+    ABI_GUARD(-1, {
+        if (!e || !out) throw HipFail{"bad arguments"};
+        *out = e->prof;
+        return 0;
+    })
+}
+
+int64_t bt_format_summaries(const bt_summary* r, int32_t P, char* out, size_t cap) {
+    ABI_GUARD(-1, {
+        if (P < 0) throw HipFail{"bad arguments"};
+        if (!out) return (int64_t)((size_t)P * kLineMax);
+        if (P > 0 && !r) throw HipFail{"bad arguments"};
+        if (cap < (size_t)P * kLineMax) throw HipFail{"output buffer too small"};
+        return (int64_t)fmt_job_into(r, P, out);
     })
 }
 

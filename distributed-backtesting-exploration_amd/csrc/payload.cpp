@@ -15,6 +15,7 @@
 //
 // Validation is the CSV path's (spec §2-§3): every price in [1, 2^31), |c_t - c_{t-1}| <=
 // c_{t-1}, exact length. Decoding is a bounds-checked copy into the engine's columns.
+#include <climits>
 #include <cstring>
 
 #include "csv.h"
@@ -95,6 +96,75 @@ bool parse_binary(const uint8_t* buf, size_t len, Bars& out, std::string& err) {
             err = "bar " + std::to_string(t) + ": close moves more than 100% in one bar";
             return false;
         }
+    }
+    return true;
+}
+
+bool binary_header(const uint8_t* buf, size_t len, int32_t& n_bars, std::string& err) {
+    if (len < 16 || !is_binary_payload(buf, len)) {
+        err = "binary payload: bad header";
+        return false;
+    }
+    const uint32_t n = rd32(buf + 8), flags = rd32(buf + 12);
+    if (n < 1 || n > (uint32_t)kMaxBars) {
+        err = "binary payload: bar count out of range";
+        return false;
+    }
+    if ((flags & ~1u) != 0) {
+        err = "binary payload: unknown flags";
+        return false;
+    }
+    if (len != binary_payload_size((int32_t)n, flags & 1)) {
+        err = "binary payload: length does not match the header";
+        return false;
+    }
+    n_bars = (int32_t)n;
+    return true;
+}
+
+// The batch ingest's decoder: validation (spec §2-§3) and the copy of the columns the strategy
+// reads (h, l may be null) into the engine's staging rows in one pass over the payload, in
+// L1-sized chunks (the payload may sit at any byte alignment; the chunks are aligned copies).
+// On a failure the message comes from parse_binary, so both paths name the same first error.
+bool decode_binary_into(const uint8_t* buf, size_t len, int32_t* h, int32_t* l, int32_t* c,
+                        std::string& err) {
+    int32_t nb = 0;
+    if (!binary_header(buf, len, nb, err)) return false;
+    const size_t n = (size_t)nb;
+    const uint8_t* col = buf + 16;
+    constexpr size_t kChunk = 2048;
+    alignas(64) int32_t sc[3][kChunk];
+    int64_t prev = 0;
+    bool bad = false;
+    for (size_t t0 = 0; t0 < n && !bad; t0 += kChunk) {
+        const size_t m = n - t0 < kChunk ? n - t0 : kChunk;
+        int32_t* po = sc[0];
+        int32_t* ph = h ? h + t0 : sc[1];
+        int32_t* pl = l ? l + t0 : sc[2];
+        int32_t* pc = c + t0;
+        memcpy(po, col + t0 * 4, m * 4);
+        memcpy(ph, col + (n + t0) * 4, m * 4);
+        memcpy(pl, col + (2 * n + t0) * 4, m * 4);
+        memcpy(pc, col + (3 * n + t0) * 4, m * 4);
+        int32_t mn = INT32_MAX;
+        for (size_t t = 0; t < m; ++t) {
+            const int32_t a = po[t] < ph[t] ? po[t] : ph[t], b = pl[t] < pc[t] ? pl[t] : pc[t];
+            const int32_t x = a < b ? a : b;
+            mn = x < mn ? x : mn;
+        }
+        // with every price >= 1, |c_t - c_{t-1}| <= c_{t-1} is c_t <= 2 c_{t-1}
+        int64_t over = t0 > 0 ? (int64_t)pc[0] - 2 * prev : INT64_MIN;
+        for (size_t t = 1; t < m; ++t) {
+            const int64_t d = (int64_t)pc[t] - 2 * (int64_t)pc[t - 1];
+            over = d > over ? d : over;
+        }
+        bad = mn < 1 || over > 0;
+        prev = pc[m - 1];
+    }
+    if (bad) {
+        Bars tmp;
+        if (parse_binary(buf, len, tmp, err)) err = "binary payload: invalid";
+        return false;
     }
     return true;
 }

@@ -41,6 +41,10 @@ from . import proto as P
 
 log = logging.getLogger("dbx_amd.dispatcher")
 
+DEFAULT_RECEIVE = 4 * 1024 * 1024   # grpcio's (and tonic's) default client receive limit
+REPLY_MARGIN = 64 * 1024            # JobsReply framing beyond the payload bytes
+JOB_OVERHEAD = 64                   # per Job: UUID string, field tags and lengths
+
 
 def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
     """main.rs:151-162, including Vec::split_off's tail semantics."""
@@ -70,6 +74,7 @@ class Dispatcher:
         self.inflight: Dict[str, tuple] = {}   # id -> (peer, path) until completed
         self.done_paths: Dict[str, str] = {}   # path -> id of its first completion
         self.requeued = 0
+        self.failed_paths: List[str] = []     # unreadable / undeliverable (counted done)
         self.done_lock = threading.Lock()
         self.results_path = results_path
         # a JobsReply larger than the server's send limit fails after its files left the queue
@@ -138,6 +143,27 @@ class Dispatcher:
                 peer["status"] = req.status
         return P.StatusReply()
 
+    def _reply_cap(self, ctx) -> int:
+        """Largest reply for this request: the server's own cap, and below the receive limit the
+        worker advertised in metadata (grpcio's default 4 MiB when it sent none), less room for
+        the message framing (per job: id, tags, lengths)."""
+        limit = DEFAULT_RECEIVE
+        for key, value in ctx.invocation_metadata() or ():
+            if key == P.MAX_RECEIVE_KEY:
+                try:
+                    limit = int(value)
+                except ValueError:
+                    pass
+        return max(1, min(self.max_reply_bytes, limit - REPLY_MARGIN))
+
+    def _drop_unreadable(self, path):
+        """An unreadable path is finished (failed): the reference silently drops it
+        (main.rs:170-172); here it is also counted done so all_done() can become true."""
+        with self.done_lock:
+            if path not in self.done_paths:
+                self.done_paths[path] = None
+                self.failed_paths.append(path)
+
     def request_jobs(self, req, ctx):
         with self.peers_lock:
             self.peers[ctx.peer()] = {"status": P.IDLE, "last_connection": time.time()}
@@ -150,18 +176,25 @@ class Dispatcher:
             ctx.abort(grpc.StatusCode.NOT_FOUND, "No more jobs available")
         jobs = []
         size = 0
+        cap = self._reply_cap(ctx)
         for i, path in enumerate(files):
             jid = str(uuid.uuid4())
             try:
                 with open(path, "rb") as f:
                     data = f.read()
             except OSError:
+                self._drop_unreadable(path)
                 continue
-            if jobs and size + len(data) > self.max_reply_bytes:
+            need = len(data) + JOB_OVERHEAD
+            if size + need > cap:
+                if not jobs and need > cap:  # can never be delivered to this worker
+                    log.error("%s (%d bytes) exceeds the worker's receive limit", path, len(data))
+                    self._drop_unreadable(path)
+                    continue
                 with self.files_lock:
                     self.files.extend(files[i:])
                 break
-            size += len(data)
+            size += need
             with self.done_lock:
                 self.job_paths[jid] = path
                 self.inflight[jid] = (ctx.peer(), path)
@@ -172,7 +205,7 @@ class Dispatcher:
 
 def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20,
           gzip: bool = True):
-    dispatcher.max_reply_bytes = min(dispatcher.max_reply_bytes, max_send - (1 << 20))
+    dispatcher.max_reply_bytes = min(dispatcher.max_reply_bytes, max_send - REPLY_MARGIN)
     ser = lambda m: m.SerializeToString()  # noqa: E731
     handlers = {
         "CompleteJob": grpc.unary_unary_rpc_method_handler(

@@ -68,6 +68,13 @@ class _JobOut(C.Structure):
                 ("n_bars", C.c_int32)]
 
 
+class _BatchProfile(C.Structure):
+    _fields_ = [("n_jobs", C.c_int64), ("n_failed", C.c_int64), ("payload_bytes", C.c_int64),
+                ("bars", C.c_int64), ("host_ingest_ms", C.c_double), ("upload_ms", C.c_double),
+                ("compute_ms", C.c_double), ("readback_ms", C.c_double),
+                ("format_ms", C.c_double), ("total_ms", C.c_double)]
+
+
 class _Stats(C.Structure):
     _fields_ = [("n_symbols", C.c_int64), ("n_params", C.c_int64), ("bar_evals", C.c_int64),
                 ("trades", C.c_int64), ("errors", C.c_int64)]
@@ -125,6 +132,9 @@ def lib():
     L.bt_encode_columns.restype = C.c_int64
     L.bt_gen_payload.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, P, C.c_size_t]
     L.bt_gen_payload.restype = C.c_int64
+    L.bt_last_batch_profile.argtypes = [P, C.POINTER(_BatchProfile)]
+    L.bt_format_summaries.argtypes = [P, C.c_int32, P, C.c_size_t]
+    L.bt_format_summaries.restype = C.c_int64
     _lib = L
     return L
 
@@ -353,12 +363,18 @@ class Engine:
             jin[i].file = C.cast(C.c_char_p(b), C.c_void_p)
             jin[i].len = len(b)
         jout = (_JobOut * max(n, 1))()
-        _check(lib().bt_run_batch(self._h, n, jin, jout))
         try:
+            _check(lib().bt_run_batch(self._h, n, jin, jout))
             res = [(jout[i].status, C.string_at(jout[i].data, jout[i].len).decode()) for i in range(n)]
         finally:
-            lib().bt_job_out_free(jout, n)
+            lib().bt_job_out_free(jout, n)  # safe on NULL entries, also after a failure
         return res
+
+    def batch_profile(self) -> dict:
+        """Phase times of the last run_batch (bt_last_batch_profile)."""
+        pr = _BatchProfile()
+        _check(lib().bt_last_batch_profile(self._h, C.byref(pr)))
+        return {f: getattr(pr, f) for f, _ in _BatchProfile._fields_}
 
 
 def merge_topk(records: np.ndarray, k: int) -> np.ndarray:
@@ -368,6 +384,15 @@ def merge_topk(records: np.ndarray, k: int) -> np.ndarray:
     m = _check(lib().bt_merge_topk(recs.ctypes.data if len(recs) else None, len(recs), k,
                                    out.ctypes.data))
     return out[:m]
+
+
+def format_summaries(rows: np.ndarray) -> str:
+    """The CompleteRequest.data text bt_run_batch writes for these summaries (spec §6)."""
+    rows = np.ascontiguousarray(rows, SUMMARY_DTYPE)
+    cap = _check(lib().bt_format_summaries(None, len(rows), None, 0))
+    buf = C.create_string_buffer(max(cap, 1))
+    n = _check(lib().bt_format_summaries(rows.ctypes.data if len(rows) else None, len(rows), buf, cap))
+    return buf.raw[:n].decode()
 
 
 def i128_to_double(lo: int, hi: int) -> float:

@@ -70,5 +70,10 @@ MESSAGES = {c.DESCRIPTOR.name: c for c in
             (JobsRequest, Job, JobsReply, CompleteRequest, CompleteReply, StatusRequest, StatusReply)}
 
 
+# gRPC metadata key (not a proto field: the contract stays byte-identical) with which a worker
+# tells the dispatcher its max receive size, so JobsReplies are capped below it
+MAX_RECEIVE_KEY = "x-dbx-max-receive"
+
+
 def method_path(name: str) -> str:
     return f"/{SERVICE}/{name}"

@@ -14,6 +14,7 @@ completion carries the results string as `data` (the reference sends `data = id`
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import os
 import queue
@@ -44,12 +45,24 @@ def engine_processor(engine) -> Processor:
 
 def process_incoming_job(jobs_reply, complete_send: "queue.Queue", processor: Processor) -> None:
     """Drop-in for `process_incoming_job` (process.rs:13-29): PROC_FLAG up, the reply's jobs
-    processed (one GPU batch), one (id, data) completion per job in job order, PROC_FLAG down."""
+    processed (one GPU batch), one (id, data) completion per job in job order, PROC_FLAG down.
+
+    An engine failure (HIP error, BtError) does not end the compute thread: every job of the
+    batch completes with one `{"error": ...}` line, as INTEGRATION.md's Rust body does, so the
+    dispatcher records the jobs instead of waiting for completions that never come (the
+    reference has no retry, README.md:82)."""
     PROC_FLAG.set()
     try:
         jobs = [(j.id, j.File) for j in jobs_reply.jobs]
         if jobs:
-            results = processor(jobs)
+            try:
+                results = list(processor(jobs))
+                if len(results) != len(jobs):
+                    raise RuntimeError(f"processor returned {len(results)} results for {len(jobs)} jobs")
+            except Exception as why:  # noqa: BLE001 — reported per job, thread stays alive
+                log.error("batch of %d jobs failed: %s", len(jobs), why)
+                msg = json.dumps({"error": f"engine failure: {why}"}) + "\n"
+                results = [msg] * len(jobs)
             for (jid, _), data in zip(jobs, results):
                 complete_send.put((jid, data))
     finally:
@@ -77,6 +90,7 @@ class Worker:
         # ... and waits up to `linger_s` for more replies while the batch holds fewer than
         # `min_batch_jobs` symbols (a launch runs one workgroup per symbol: hundreds fill it)
         self.min_batch_jobs, self.linger_s = min_batch_jobs, linger_s
+        self.max_receive = max_receive
         opts = [("grpc.max_receive_message_length", max_receive)]
         self.channel = grpc.insecure_channel(target, options=opts)
         u = self.channel.unary_unary
@@ -128,7 +142,10 @@ class Worker:
                 log.error("Unable to send status: %s", why)
             CONNECTED.clear()
         try:
-            reply = self._request(P.JobsRequest(cores=self.cores))
+            # the receive limit travels as metadata (the proto stays unchanged): the dispatcher
+            # caps the reply below it instead of sending one this channel would refuse
+            reply = self._request(P.JobsRequest(cores=self.cores),
+                                  metadata=((P.MAX_RECEIVE_KEY, str(self.max_receive)),))
         except grpc.RpcError:
             return  # empty queue / server gone: the reference ignores it (handlers.rs:59)
         self.reply_q.put(reply)

@@ -132,10 +132,26 @@ const char* bt_last_error(void);      /* thread-local message of the last failed
 int32_t bt_abi_version(void);
 int32_t bt_num_params(const bt_engine* e);
 
+/* Phase times of the last bt_run_batch call (host clocks for host phases, HIP events for the
+ * device ones). */
+typedef struct bt_batch_profile {
+    int64_t n_jobs, n_failed;
+    int64_t payload_bytes;            /* sum of Job.File lengths */
+    int64_t bars;                     /* bars of the good jobs */
+    double host_ingest_ms;            /* parse / validate + copy into pinned staging */
+    double upload_ms;                 /* H2D of the staged columns */
+    double compute_ms;                /* strategy kernel (+ top-k when enabled) */
+    double readback_ms;               /* one D2H of every summary of the batch */
+    double format_ms;                 /* CompleteRequest.data strings */
+    double total_ms;                  /* wall time of the call */
+} bt_batch_profile;
+
 /* ---- drop-in for process_incoming_job: a whole JobsReply in one GPU launch.
- * outs[i] answers jobs[i] (same order the reference sends completions, process.rs:21-25). */
+ * outs[i] answers jobs[i] (same order the reference sends completions, process.rs:21-25).
+ * On a -1 return no output string is left allocated (outs are all NULL). */
 int32_t bt_run_batch(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* outs);
 void bt_job_out_free(bt_job_out* outs, size_t n);
+int32_t bt_last_batch_profile(bt_engine* e, bt_batch_profile* out);
 
 /* ---- HBM-resident path (configs 2-5, bench, multi-GPU shards) */
 /* Generate n_sym synthetic symbols (spec §1) with ids sym_begin.. directly in HBM. */
@@ -176,6 +192,9 @@ int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n);
 int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* out);
 
 /* ---- self-test hooks (host-side helpers the tests call without a GPU) */
+/* The CompleteRequest.data text of P summaries (spec §6, one JSON line per param), as
+ * bt_run_batch writes it; returns its length, or the capacity needed when out is NULL. */
+int64_t bt_format_summaries(const bt_summary* r, int32_t P, char* out, size_t cap);
 double bt_i128_to_double(uint64_t lo, int64_t hi);
 int32_t bt_parse_csv(const uint8_t* buf, size_t len, int32_t cap, int32_t* h, int32_t* l,
                      int32_t* c, char* err, size_t errlen);   /* same as bt_parse_job */

@@ -126,3 +126,27 @@ def test_release_library_reads_no_environment():
     out = subprocess.run(["nm", "-D", "--undefined-only", E.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     assert not re.search(r"\bgetenv\b", out)
+
+
+def test_result_lines_match_printf_format():
+    """bt_run_batch's CompleteRequest.data lines (std::to_chars) are byte-identical to the spec §6
+    printf format: "%.17g" Sharpe, "%016x" hash, decimal integers."""
+    rng = np.random.default_rng(7)
+    n = 3000
+    rows = np.zeros(n, D.SUMMARY_DTYPE)
+    rows["n_trades"] = rng.integers(0, 2**31 - 1, n)
+    rows["pnl"] = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    rows["mdd"] = rng.integers(0, 2**63 - 1, n, dtype=np.int64)
+    rows["exposure"] = rng.integers(0, 2**22, n)
+    sh = rng.standard_normal(n) * 10.0 ** rng.integers(-300, 300, n)
+    sh[:8] = [0.0, -0.0, 1.0, -1.5, 1e-320, 5e-324, 1.7976931348623157e308, 0.1]
+    rows["sharpe"] = sh
+    rows["hash"] = rng.integers(0, 2**63, n, dtype=np.uint64) * 2 + rng.integers(0, 2, n).astype(np.uint64)
+    rows["hash"][0] = 0
+    got = E.format_summaries(rows).split("\n")
+    assert got[-1] == "" and len(got) == n + 1
+    for p, (r, line) in enumerate(zip(rows, got)):
+        exp = ('{"param":%d,"n":%d,"pnl":%d,"mdd":%d,"exp":%d,"sharpe":"%.17g","h":"%016x"}'
+               % (p, r["n_trades"], r["pnl"], r["mdd"], r["exposure"], r["sharpe"], r["hash"]))
+        assert line == exp, (p, line, exp)
+        assert json.loads(line)["param"] == p

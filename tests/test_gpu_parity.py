@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import dbx_amd as D
+from dbx_amd import engine as E
 import orc_ffi as F
 from helpers import compare_summary, compare_trades, oracle_row
 
@@ -391,3 +392,44 @@ def test_boll_many_k_values():
             where = f"boll 12 k sym {s} {grid.param(p)}"
             compare_summary(got[s, p], orc[p], where)
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+def test_run_batch_binary_and_csv_mixed():
+    """bt_run_batch on one JobsReply mixing DBXCOL1 payloads (decoded straight into the pinned
+    staging rows), CSV text, and malformed payloads of every kind: good jobs bit-exact vs the
+    oracle (Bollinger: high/low columns too), bad jobs answered with the same message the
+    standalone parser gives, and the batch profile accounts for every job."""
+    import json
+    import oracle_np as N
+    from dbx_amd import payload as PL
+    grid = D.Grid.boll([10, 45], [3, 5], [50, 100], [100, 400], k_den=2)
+    o, h, lo, c, v = N.gen(0x5EED, [0, 1, 2], 3000, 1)
+    good = {0: PL.encode_columns(o[0], h[0], lo[0], c[0], v[0]),
+            2: N.csv_bytes(o[1], h[1], lo[1], c[1], v[1], 1),
+            4: PL.encode_columns(o[2], h[2], lo[2], c[2])}
+    base = PL.encode_columns(o[0][:100], h[0][:100], lo[0][:100], c[0][:100])
+    bad = {1: base[:-1],                                                          # length
+           3: base[:16 + 4 * 300 + 8] + (0).to_bytes(4, "little") + base[16 + 4 * 300 + 12:],  # price
+           5: base[:16 + 4 * 300 + 40] + (2**31 - 1).to_bytes(4, "little") + base[16 + 4 * 300 + 44:]}  # 100%
+    jobs = [(f"j{i}", good[i] if i in good else bad[i]) for i in range(6)]
+    with D.Engine(grid) as e:
+        res = e.run_batch(jobs)
+        prof = e.batch_profile()
+        st = e.stats()
+    assert prof["n_jobs"] == 6 and prof["n_failed"] == 3 and st["errors"] == 3
+    assert prof["bars"] == 9000 and prof["payload_bytes"] == sum(len(b) for _, b in jobs)
+    for i, b in bad.items():
+        assert res[i][0] < 0
+        with pytest.raises(ValueError) as why:
+            E.parse_csv(b)
+        assert json.loads(res[i][1])["error"] == str(why.value)
+    for i, s in ((0, 0), (2, 1), (4, 2)):
+        status, data = res[i]
+        assert status == 0
+        lines = data.strip().split("\n")
+        orc, _ = oracle_row("boll", grid, (o[s], h[s], lo[s], c[s]), 98280)
+        for p, line in enumerate(lines):
+            j = json.loads(line)
+            assert j["n"] == int(orc[p]["n_trades"]) and j["pnl"] == int(orc[p]["pnl"])
+            assert j["mdd"] == int(orc[p]["mdd"]) and j["exp"] == int(orc[p]["exposure"])
+            assert float(j["sharpe"]) == float(orc[p]["sharpe"]) and int(j["h"], 16) == int(orc[p]["hash"])

@@ -158,11 +158,15 @@ def test_process_incoming_job_flag_and_order():
 
 class _Ctx:
     """Minimal grpc ServicerContext stand-in for direct handler calls."""
-    def __init__(self, peer):
+    def __init__(self, peer, metadata=()):
         self._peer = peer
+        self._md = tuple(metadata)
 
     def peer(self):
         return self._peer
+
+    def invocation_metadata(self):
+        return self._md
 
     def abort(self, code, msg):
         raise RuntimeError(msg)

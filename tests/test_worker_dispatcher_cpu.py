@@ -1,0 +1,144 @@
+"""Worker / dispatcher counterparts on the CPU, without a server:
+reply merging on the compute thread, engine failures answered per job, receive-limit-aware
+reply caps, unreadable paths counted as finished."""
+import json
+import queue
+import threading
+import time
+
+from dbx_amd import dispatcher as DSP
+from dbx_amd import proto as P
+from dbx_amd import worker as WK
+from test_grpc_harness import _Ctx
+
+
+def _reply(ids, size=10):
+    return P.JobsReply(jobs=[P.Job(id=str(i), File=b"x" * size) for i in ids])
+
+
+def _run_compute(w, replies, wait_jobs, timeout=5.0):
+    """Feed replies to the worker's compute thread (main.rs:38-42) and collect completions."""
+    for r in replies:
+        w.reply_q.put(r)
+    th = threading.Thread(target=w._compute, daemon=True)
+    th.start()
+    got = []
+    t0 = time.time()
+    while len(got) < wait_jobs and time.time() - t0 < timeout:
+        try:
+            got.append(w.complete_q.get(timeout=0.05))
+        except queue.Empty:
+            pass
+    w.stop.set()
+    th.join(2)
+    return got
+
+
+def test_reply_merging_batches_queued_replies_in_order():
+    """f2: with max_batch_bytes the compute thread merges the JobsReplies already queued into one
+    engine batch (one launch), up to the byte budget, keeping job order."""
+    calls = []
+
+    def proc(jobs):
+        calls.append([j for j, _ in jobs])
+        return [f"r{j}" for j, _ in jobs]
+    w = WK.Worker("127.0.0.1:1", proc, cores=2, max_batch_bytes=45)
+    got = _run_compute(w, [_reply([0, 1]), _reply([2, 3]), _reply([4, 5]), _reply([6])], 7)
+    assert [g[0] for g in got] == [str(i) for i in range(7)]
+    assert [g[1] for g in got] == [f"r{i}" for i in range(7)]
+    # 20 B per reply: the first batch stops once it holds >= 45 B (three replies)
+    assert calls[0] == ["0", "1", "2", "3", "4", "5"] and calls[1] == ["6"]
+
+
+def test_reply_merging_lingers_for_min_batch_jobs():
+    """f2: while a batch holds fewer than min_batch_jobs symbols the thread waits linger_s for
+    another reply instead of launching a nearly empty grid."""
+    calls = []
+
+    def proc(jobs):
+        calls.append(len(jobs))
+        return ["ok"] * len(jobs)
+    w = WK.Worker("127.0.0.1:1", proc, cores=2, max_batch_bytes=1 << 20, min_batch_jobs=4,
+                  linger_s=0.5)
+
+    def late():
+        time.sleep(0.15)
+        w.reply_q.put(_reply([2, 3]))
+    threading.Thread(target=late, daemon=True).start()
+    got = _run_compute(w, [_reply([0, 1])], 4)
+    assert len(got) == 4 and calls == [4]
+
+
+def test_without_merging_one_reply_per_call():
+    calls = []
+
+    def proc(jobs):
+        calls.append(len(jobs))
+        return ["ok"] * len(jobs)
+    w = WK.Worker("127.0.0.1:1", proc, cores=2)
+    _run_compute(w, [_reply([0, 1]), _reply([2])], 3)
+    assert calls == [2, 1]                               # main.rs:38-42: one reply per call
+
+
+def test_engine_failure_completes_every_job_with_an_error():
+    """An exception in the processor (HIP error, BtError) must not end the compute thread: every
+    job of the batch completes with {"error": ...} and later batches still run."""
+    n = {"calls": 0}
+
+    def proc(jobs):
+        n["calls"] += 1
+        if n["calls"] == 1:
+            raise RuntimeError("hipErrorLaunchFailure")
+        return ["fine"] * len(jobs)
+    w = WK.Worker("127.0.0.1:1", proc, cores=2)
+    got = _run_compute(w, [_reply([0, 1, 2]), _reply([3])], 4)
+    assert [g[0] for g in got] == ["0", "1", "2", "3"]
+    for _, data in got[:3]:
+        assert "hipErrorLaunchFailure" in json.loads(data)["error"]
+    assert got[3][1] == "fine" and not WK.PROC_FLAG.is_set()
+
+
+def test_processor_with_wrong_result_count_is_an_error():
+    q = queue.Queue()
+    WK.process_incoming_job(_reply([0, 1]), q, lambda jobs: ["only one"])
+    assert [q.get_nowait()[0] for _ in range(2)] == ["0", "1"]
+
+
+def test_reply_capped_below_worker_receive_limit(tmp_path):
+    """The worker advertises its receive limit in metadata; the dispatcher keeps replies below
+    it (less framing) so a reply is never refused after its files left the queue."""
+    paths = [str(tmp_path / f"f{i}") for i in range(8)]
+    for p in paths:
+        open(p, "wb").write(b"x" * 30000)
+    d = DSP.Dispatcher(paths)
+    try:
+        md = ((P.MAX_RECEIVE_KEY, str(DSP.REPLY_MARGIN + 100000)),)
+        r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))     # all 8 asked for
+        assert len(r.jobs) == 3                                       # 3 x (30000 + 64) fit
+        assert len(r.SerializeToString()) < DSP.REPLY_MARGIN + 100000
+        r2 = d.request_jobs(P.JobsRequest(cores=0), _Ctx("b"))        # default 4 MiB: the rest
+        assert len(r2.jobs) == 5 and not d.files
+    finally:
+        d.close()
+
+
+def test_unreadable_and_undeliverable_paths_count_as_finished(tmp_path):
+    good = tmp_path / "good"
+    good.write_bytes(b"2020-01-01,1,1,1,1,1\n")
+    big = tmp_path / "big"
+    big.write_bytes(b"y" * 5000)
+    paths = [str(tmp_path / "missing"), str(good), str(big)]
+    d = DSP.Dispatcher(paths)
+    try:
+        md = ((P.MAX_RECEIVE_KEY, str(DSP.REPLY_MARGIN + 1000)),)
+        r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))
+        assert [d.job_paths[j.id] for j in r.jobs] == [str(good)]
+        assert d.failed_paths == [str(tmp_path / "missing")] and d.files == [str(big)]
+        r2 = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))   # big alone cannot fit
+        assert len(r2.jobs) == 0 and not d.files
+        assert sorted(d.failed_paths) == sorted([str(tmp_path / "missing"), str(big)])
+        assert not d.all_done()
+        d.complete_job(P.CompleteRequest(id=r.jobs[0].id, data="ok"), _Ctx("a"))
+        assert d.all_done()                                           # --exit-when-done ends
+    finally:
+        d.close()
