@@ -1,20 +1,27 @@
 """bench.py — bar-evals/s of the backtest hot path on 1..N MI355X (BASELINE.json metric).
 
-Default workload (N=1 and per GPU for N>1): BASELINE config 2 — SMA fast/slow crossover,
-5,000 symbols x 2,520 daily bars x 400 param pairs, synthetic OHLC (docs/oracle_spec.md §1)
-generated directly in HBM before timing. One step = one pass of the hot path over that batch:
-the fused strategy kernel (indicators + signals + position/PnL/drawdown/Sharpe per lane), the
-per-GPU top-k and its read-back; for N>1 also one RCCL all-gather of every rank's top-k records
-and counters (the only exchange step). Step i+1 is enqueued before step i's
-read-back/exchange is consumed, so host work and the collective overlap the next pass. Symbols
-are sharded across ranks with no data-path collective (weak scaling: every rank runs its own
-shard).
+Default workload (the driver's line): BASELINE config 2 — SMA fast/slow crossover, 5,000 symbols
+x 2,520 daily bars x 400 param pairs per GPU (weak scaling: config 2 is a one-GPU config, so N
+GPUs run N such shards), synthetic OHLC (docs/oracle_spec.md §1) generated directly in HBM
+before timing. One step = one pass of the hot path over that batch: the fused strategy kernel
+(indicators + signals + position/PnL/drawdown/Sharpe per lane), the per-GPU top-k and its
+read-back; for N > 1 also the exchange step: ONE RCCL all-gather of every
+rank's top-k records and counters, issued through the C ABI (bt_exchange_async, csrc/comm.cpp)
+straight from the engine's device buffers. Step i+1 is enqueued before step i's read-back /
+exchange is consumed, so host work and the collective overlap the next pass.
 
-`--config 3|4|5` measures the per-GPU shard of the other BASELINE configs the same way (EMA+OLS
-500 x 98,280 x 64; Bollinger 500 x 98,280 x 256, i.e. 2,000 symbols over 4 GPUs; SMA
-1,250 x 491,400 x 1,024, i.e. 10,000 symbols over 8 GPUs); the driver runs the default.
+`--config 3|4|5` runs BASELINE's other configs with STRONG scaling by default: the pinned
+totals (config 3: 500 symbols x 98,280 1-min bars x 64 params, quoted at 1 and 2 GPUs; config 4:
+2,000 x 98,280 x 256 at 4 and 8 GPUs; config 5: 10,000 x 491,400 x 1,024 at 8 GPUs) are split
+into contiguous symbol shards (parallel.shard), so `--gpus 8 --config 4` runs 250 symbols per
+rank. `--scaling weak` keeps the per-GPU shard fixed instead (config 4: 500 per GPU).
 
-Run: python bench.py [--gpus N --steps K --warmup W] [--config C]
+`--leg ingest` times the engine's own share of a gRPC-fed run instead: bt_run_batch (the
+drop-in for process_incoming_job) on 256 config-5 symbols as DBXCOL1 payloads in host memory —
+payload validation and staging, H2D, the kernel, the summaries' read-back and the
+CompleteRequest.data strings — and prints its own JSON line.
+
+Run: python bench.py [--gpus N --steps K --warmup W] [--config C] [--scaling weak|strong]
      torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 from __future__ import annotations
@@ -39,18 +46,25 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (MI355X_MICROARCH.md per-instruction constants: v_fma_f32 wave64 = 2 cycles on SIMD-32)
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
 
-# per-GPU shard of each BASELINE config: grid, symbols, bars, bar frequency, annualization,
-# and the SURVEY.md §8(d) byte-model terms c (OHLC columns consumed) and W (indicator series)
+# BASELINE configs: grid, symbols (per GPU for weak scaling, the pinned total for strong), bars,
+# bar frequency, annualization, default scaling, and the SURVEY.md §8(d) byte-model terms c (OHLC
+# columns consumed) and W (indicator series)
 CONFIGS = {
     2: dict(grid=D.config2_grid, S=5000, B=2520, freq=D.BT_DAILY, ann=252, c=1, W=40,
-            name="BASELINE config 2: SMA fast/slow crossover"),
+            scaling="weak", name="BASELINE config 2: SMA fast/slow crossover, 5,000 symbols x "
+            "2,520 daily bars x 400 params per GPU"),
     3: dict(grid=D.config3_grid, S=500, B=98280, freq=D.BT_MINUTE, ann=98280, c=1, W=16,
-            name="BASELINE config 3: EMA + rolling-OLS-slope mean reversion"),
-    4: dict(grid=D.config4_grid, S=500, B=98280, freq=D.BT_MINUTE, ann=98280, c=3, W=16,
-            name="BASELINE config 4: Bollinger z-score with SL/TP (2,000 symbols over 4 GPUs)"),
-    5: dict(grid=D.config5_grid, S=1250, B=491400, freq=D.BT_MINUTE, ann=98280, c=1, W=64,
-            name="BASELINE config 5: SMA 32x32 grid, 5y 1-min bars (10,000 symbols over 8 GPUs)"),
+            scaling="strong", name="BASELINE config 3: EMA + rolling-OLS-slope mean reversion, "
+            "500 symbols x 98,280 1-min bars x 64 params in total"),
+    4: dict(grid=D.config4_grid, S=2000, B=98280, freq=D.BT_MINUTE, ann=98280, c=3, W=16,
+            scaling="strong", name="BASELINE config 4: Bollinger z-score with SL/TP, 2,000 "
+            "symbols x 98,280 1-min bars x 256 params in total"),
+    5: dict(grid=D.config5_grid, S=10000, B=491400, freq=D.BT_MINUTE, ann=98280, c=1, W=64,
+            scaling="strong", name="BASELINE config 5: SMA 32x32 grid, 10,000 symbols x 491,400 "
+            "1-min bars (5 y) x 1,024 params in total"),
 }
+# the per-GPU shard the weak-scaling mode keeps for configs 3/4/5 (round-1 shard sizes)
+WEAK_SHARD = {2: 5000, 3: 500, 4: 500, 5: 1250}
 
 
 def algorithmic_bytes(S, B, P, c=1, W=40):
@@ -58,27 +72,60 @@ def algorithmic_bytes(S, B, P, c=1, W=40):
     return S * B * (8 * c + 16 * W) + 32 * S * P
 
 
-def cpu_baseline(cfg, grid, threads=None, target_thread_s=25.0):
+def host_cpus():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota if any (the
+    GPU box gives a job a share of a large host: nproc shows the whole machine)."""
+    nproc = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, period = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+        except (OSError, ValueError):
+            pass
+    usable = max(1, min(aff, int(quota) if quota else aff))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable,
+            "model": model}
+
+
+def cpu_baseline(cfg, grid, sym0, shard, target_thread_s=25.0, target_1t_s=8.0):
     """The C oracle (oracle/oracle.c, -O2 -ffp-contract=off) on the first symbols of
-    the same workload, sized from a one-symbol probe to ~target_thread_s thread-seconds. SMA
-    grids run on the oracle's pthread grid (one symbol per thread); EMA/Bollinger run one
-    (symbol, param) call per task on a thread pool (ctypes releases the GIL)."""
+    rank 0's shard of the same workload, on 1 thread and on every usable host CPU, each sample
+    sized from a one-symbol probe (~8 s on one thread, ~25 thread-seconds on all). SMA grids run
+    on the oracle's pthread grid (one symbol per task); EMA/Bollinger run one (symbol, param)
+    call per task on a thread pool (ctypes releases the GIL)."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc_ffi as F
-    threads = threads or min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
     B, freq, ann = cfg["B"], 1 if cfg["freq"] == D.BT_MINUTE else 0, cfg["ann"]
+    cache = {}
 
-    def run(n):
-        cols = [F.gen(SEED, s, B, freq) for s in range(n)]
+    def cols(n):
+        for s in range(len(cache), n):
+            cache[s] = F.gen(SEED, sym0 + s, B, freq)
+        return [cache[s] for s in range(n)]
+
+    def run(n, threads):
+        cs = cols(n)
         t0 = time.perf_counter()
         if grid.strategy == D.BT_SMA_CROSS:
-            F.sma_grid_mt(np.stack([x[3] for x in cols]), np.asarray(grid.axes[0]),
+            F.sma_grid_mt(np.stack([x[3] for x in cs]), np.asarray(grid.axes[0]),
                           np.asarray(grid.axes[1]), ann, threads)
         else:
             def one(sp):
                 s, p = sp
-                o, h, lo, c = cols[s][:4]
+                o, h, lo, c = cs[s][:4]
                 kw = grid.param(p)
                 if grid.strategy == D.BT_EMA_OLS:
                     F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], ann)
@@ -88,55 +135,32 @@ def cpu_baseline(cfg, grid, threads=None, target_thread_s=25.0):
                 list(ex.map(one, [(s, p) for s in range(n) for p in range(grid.n_params)]))
         return time.perf_counter() - t0
 
-    probe = min(threads, cfg["S"]) if grid.strategy == D.BT_SMA_CROSS else 1
-    dt = run(probe)
-    thread_s = dt * (threads if grid.strategy != D.BT_SMA_CROSS else min(threads, probe))
-    per_sym = thread_s / probe
-    n_sym = int(min(cfg["S"], max(probe, target_thread_s / max(per_sym, 1e-9))))
-    if n_sym > probe:
-        dt = run(n_sym)
-    else:
-        n_sym = probe
-    evals = n_sym * B * grid.n_params
-    return {"value": evals / dt, "unit": "bar-evals/s", "cores": threads, "kind": "port",
-            "sample": f"first {n_sym} of the {cfg['S']} shard symbols x {B} bars x "
-                      f"{grid.n_params} params ({evals:.3g} bar-evals, {dt:.2f} s wall = "
-                      f"{dt * threads:.1f} thread-s on {threads} threads; oracle/oracle.c, gcc -O2 -ffp-contract=off)"}
+    per_sym = run(1, 1)  # one symbol on one thread: the probe
+    n1 = int(min(shard, max(1, target_1t_s / max(per_sym, 1e-9))))
+    dt1 = run(n1, 1) if n1 > 1 else per_sym
+    T = cpus["usable"]
+    nA = int(min(shard, max(T, target_thread_s / max(per_sym, 1e-9))))
+    dtA = run(nA, T)
+    per_eval = B * grid.n_params
+    v1, vA = n1 * per_eval / dt1, nA * per_eval / dtA
+    return {"value": vA, "unit": "bar-evals/s", "cores": T, "kind": "port",
+            "sample": f"first {nA} symbols of the shard x {B} bars x {grid.n_params} params on "
+                      f"{T} threads ({dtA:.2f} s wall); 1 thread: first {n1} symbols ({dt1:.2f} s); "
+                      f"oracle/oracle.c, gcc -O2 -ffp-contract=off",
+            "value_1t": v1, "value_all": vA, "threads_all": T, "nproc": cpus["nproc"],
+            "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
+            "model": cpus["model"]}
 
 
-def load_traffic(config):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summaries."""
-    path = os.path.join(ROOT, "profiles", "pmc_sma_config2.json") if config == 2 else \
-        os.path.join(ROOT, "profiles", "r01_configs", "configs.json")
+def load_pmc(config):
+    """Measured HBM bytes and VALU instructions per launch of the dominant kernel from the
+    committed rocprofv3 PMC summaries (profiles/pmc_config<C>.json, written by
+    scripts/summarize_profile.py from separate --pmc passes of this same bench command)."""
     try:
-        d = json.load(open(path))
-        if config == 2:
-            return float(d["hbm_bytes_per_launch"])
-        v = d[f"config{config}"]
-        return float(v["hbm_read_bytes"] + v["hbm_write_bytes"])
-    except Exception:
-        return None
-
-
-def load_valu_insts(config):
-    """VALU wave-instructions per launch of the dominant kernel (PMC SQ_INSTS_VALU) from the
-    committed rocprofv3 summaries: the kernels are VALU-issue bound, not HBM bound."""
-    try:
-        if config == 2:
-            d = json.load(open(os.path.join(ROOT, "profiles", "r01", "pmc_summary.json")))
-            return float(d["sq"]["SQ_INSTS_VALU"])
-        d = json.load(open(os.path.join(ROOT, "profiles", "r01_configs", "configs.json")))
-        return float(d[f"config{config}"]["pmc"]["SQ_INSTS_VALU"])
-    except Exception:
-        return None
-
-
-def valu_issue(insts, kernel_s):
-    if insts is None:
-        return None
-    achieved = insts / kernel_s / 1e9
-    return {"insts_per_launch": insts, "achieved": achieved, "peak": VALU_PEAK_GINST,
-            "unit": "Ginst/s", "frac": achieved / VALU_PEAK_GINST}
+        d = json.load(open(os.path.join(ROOT, "profiles", f"pmc_config{config}.json")))
+        return d
+    except (OSError, ValueError):
+        return {}
 
 
 def main():
@@ -145,21 +169,36 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="default: weak for config 2, strong (BASELINE totals) for 3/4/5")
+    ap.add_argument("--symbols", type=int, default=None,
+                    help="override: symbols per GPU (weak) or in total (strong)")
+    ap.add_argument("--leg", choices=["kernel", "ingest"], default="kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.leg == "ingest":
+        return ingest_leg(args)
     cfg = CONFIGS[args.config]
-    S_PER_GPU, BARS = cfg["S"], cfg["B"]
+    scaling = args.scaling or cfg["scaling"]
+    BARS = cfg["B"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if scaling == "weak":
+        per = args.symbols or WEAK_SHARD[args.config]
+        sym0, n_sym, total = rank * per, per, per * world
+    else:
+        total = args.symbols or cfg["S"]
+        sym0, n_sym = PAR.shard(total, world, rank)
     dist = None
+    comm = None
     device = local
     if world > 1:
         import torch
         import torch.distributed as dist
         # one process per GPU; ranks outnumbering the visible GPUs (a rehearsal on a 1-GPU box)
-        # share devices, and RCCL needs distinct devices, so the k x 24 B exchange then uses gloo
+        # share devices, and RCCL needs distinct devices, so the exchange then uses gloo
         ndev = torch.cuda.device_count()
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
         device = local % max(ndev, 1)
@@ -172,19 +211,35 @@ def main():
     grid = cfg["grid"]()
     P = grid.n_params
     eng = D.Engine(grid, device=device, topk=TOPK, timing=True)
-    eng.load_synthetic(SEED, rank * S_PER_GPU, S_PER_GPU, BARS, cfg["freq"])
+    eng.load_synthetic(SEED, sym0, n_sym, BARS, cfg["freq"])
+    exchange = "none"
+    if dist is not None:
+        if dist.get_backend() == "nccl":
+            try:  # the C-ABI exchange (RCCL from the engine's device buffers)
+                comm = PAR.make_comm(dist, device, TOPK)
+                exchange = "RCCL all-gather via bt_exchange (C ABI)"
+            except Exception as why:  # noqa: BLE001 — fall back to torch's RCCL all-gather
+                print(f"bt_comm unavailable ({why}); exchanging over torch.distributed", file=sys.stderr)
+        if comm is None:
+            exchange = f"{dist.get_backend()} all-gather via torch.distributed"
 
     def issue(i):
         eng.run()                      # kernels of step i, enqueued on the engine stream
-        eng.topk_fetch_async(i & 1)    # its top-k + trade count into pinned slot i % 2
+        if comm is not None:
+            comm.exchange_async(eng, i & 1)   # RCCL all-gather behind the run's top-k chain
+        else:
+            eng.topk_fetch_async(i & 1)       # its top-k + trade count into pinned slot i % 2
 
     def finish(i):
+        if comm is not None:
+            top, _ = comm.exchange_wait(i & 1)
+            return top
         top, trades = eng.topk_fetch_wait(i & 1)
         if dist is None:
             return top
-        # the one exchange step: a single RCCL all-gather carrying each rank's k x 24 B top-k
-        # records and its run counters (summed on the host)
-        top, _ = PAR.exchange(top, TOPK, [S_PER_GPU * BARS * P, trades], dist)
+        # the one exchange step: a single all-gather carrying each rank's k x 24 B top-k records
+        # and its run counters (summed on the host)
+        top, _ = PAR.exchange(top, TOPK, [n_sym * BARS * P, trades], dist)
         return top
 
     def steps(n):
@@ -222,12 +277,17 @@ def main():
     stats = eng.stats()
 
     if rank == 0:
-        evals_per_step = S_PER_GPU * BARS * P * world
+        evals_per_step = total * BARS * P
         value = evals_per_step * args.steps / elapsed
         kavg_s = kms / 1e3 / max(launches, 1)
-        alg = algorithmic_bytes(S_PER_GPU, BARS, P, cfg["c"], cfg["W"])
+        alg = algorithmic_bytes(n_sym, BARS, P, cfg["c"], cfg["W"])
         achieved = alg / kavg_s / 1e9
-        traffic = load_traffic(args.config)
+        pmc = load_pmc(args.config)
+        # measured traffic applies to the shard it was profiled on
+        same_shard = pmc.get("symbols") == n_sym
+        traffic = pmc.get("hbm_bytes_per_launch") if same_shard else None
+        valu = pmc.get("SQ_INSTS_VALU") if same_shard else None
+        valu_frac = (valu / kavg_s / 1e9 / VALU_PEAK_GINST) if valu else None
         line = {
             "metric": "bar-evals/sec (symbols x params x bars)",
             "value": value,
@@ -237,32 +297,82 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64+int64",
             "data": "synthetic (SplitMix64 integer OHLC walk, docs/oracle_spec.md §1, generated in HBM)",
-            "config": {"workload": cfg["name"],
-                       "symbols_per_gpu": S_PER_GPU, "bars": BARS, "params": P,
-                       "topk": TOPK, "parallelism": f"dp{world} (symbol shards, "
-                       f"{'RCCL' if dist is None or dist.get_backend() == 'nccl' else 'gloo'} top-k gather)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "config": {"workload": cfg["name"] if scaling == cfg["scaling"] and args.symbols is None
+                       else f"{cfg['name'].split(':')[0]}: {total} symbols in total, {scaling} scaling",
+                       "symbols_total": total, "symbols_per_gpu": n_sym, "bars": BARS, "params": P,
+                       "topk": TOPK, "parallelism": f"dp{world} (contiguous symbol shards; "
+                       f"exchange: {exchange})"},
+            # The fused kernels move far fewer bytes than the pinned two-stage model charges, so
+            # they are not HBM-bound: achieved/frac are the SURVEY.md §8(d) model (B_alg / kernel
+            # time, the number BASELINE asks for); traffic/traffic_GBps are the measured PMC
+            # bytes; the binding limit is VALU issue/latency (valu_issue_frac).
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "model": "SURVEY.md §8(d) pinned bytes B_alg = S*B*(8c+16W) + 32*S*P",
+                         "alg_bytes_per_launch": alg,
                          "traffic": traffic,
-                         "kernel": kname, "kernel_avg_ms": kavg_s * 1e3,
-                         "alg_bytes_per_launch": alg},
-            # the bound that actually limits the fused kernels: VALU issue (PMC instruction
-            # count per launch from profiles/, over the live kernel time)
-            "valu_issue": valu_issue(load_valu_insts(args.config), kavg_s),
+                         "traffic_GBps": traffic / kavg_s / 1e9 if traffic else None,
+                         "traffic_frac": traffic / kavg_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+                         "valu_insts_per_launch": valu,
+                         "valu_issue_frac": valu_frac,
+                         "pmc_source": pmc.get("source") if same_shard else None,
+                         "kernel": kname, "kernel_avg_ms": kavg_s * 1e3},
             "trades_per_step": stats["trades"],
             "top1": {"sharpe": float(top[0]["sharpe"]), "sym": int(top[0]["sym"]),
-                     "param": int(top[0]["param"])} if len(top) else None,
+                     "param": int(top[0]["param"])} if top is not None and len(top) else None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(cfg, grid)
+            line["cpu_baseline"] = cpu_baseline(cfg, grid, sym0, n_sym)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def ingest_leg(args):
+    """bt_run_batch alone on host-resident DBXCOL1 payloads of config-5 symbols (SURVEY.md §8(f)
+    rows 1-2): the engine's share of a gRPC-fed run, without the gRPC transport."""
+    from concurrent.futures import ThreadPoolExecutor
+    from dbx_amd import payload as PL
+    cfg = CONFIGS[5]
+    n_jobs = args.symbols or 256
+    grid = cfg["grid"]()
+    with ThreadPoolExecutor(16) as ex:
+        payloads = list(ex.map(lambda s: PL.gen_payload(SEED, s, cfg["B"], cfg["freq"]), range(n_jobs)))
+    jobs = [(f"job-{s}", b) for s, b in enumerate(payloads)]
+    eng = D.Engine(grid, device=0)
+    for _ in range(max(args.warmup, 1)):
+        eng.run_batch(jobs)
+    profs, walls = [], []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        res = eng.run_batch(jobs)
+        walls.append(time.perf_counter() - t0)
+        profs.append(eng.batch_profile())
+    assert all(st == 0 for st, _ in res)
+    med = {k: float(np.median([p[k] for p in profs])) for k in profs[0] if k.endswith("_ms")}
+    pb, bars = profs[0]["payload_bytes"], profs[0]["bars"]
+    wall = float(np.median(walls))
+    line = {
+        "leg": "bt_run_batch on DBXCOL1 payloads (engine share of a gRPC-fed run)",
+        "workload": f"{n_jobs} config-5 symbols x {cfg['B']} 1-min bars x {grid.n_params} params",
+        "jobs": n_jobs, "payload_bytes": pb, "result_bytes": sum(len(d) for _, d in res),
+        "steps": args.steps, "phase_ms_median": med, "call_wall_ms_median": wall * 1e3,
+        "ingest_GBps": pb / ((med["host_ingest_ms"] + med["upload_ms"]) * 1e6),
+        "host_ingest_GBps": pb / (med["host_ingest_ms"] * 1e6),
+        "upload_GBps": bars * 4 / (med["upload_ms"] * 1e6),
+        "bar_evals_per_s_end_to_end": bars * grid.n_params / wall,
+        "bar_evals_per_s_kernel": bars * grid.n_params / (med["compute_ms"] * 1e-3),
+        "host_threads": min(16, os.cpu_count() or 1),
+    }
+    print(json.dumps(line), flush=True)
+    eng.close()
 
 
 if __name__ == "__main__":

@@ -70,6 +70,8 @@ uint32_t next_pow2(uint32_t x) {
 
 }  // namespace
 
+void bt::set_last_error(const std::string& s) { set_err(s); }
+
 struct bt_engine {
     bt_config cfg{};
     std::vector<int32_t> ax[4];  // owned copies of the grid axes
@@ -380,12 +382,6 @@ void drain_timing(bt_engine* e) {
     e->ev_pending.clear();
 }
 
-bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b) {  // "a ranks before b"
-    const uint64_t ka = order_key(a.sharpe), kb = order_key(b.sharpe);
-    if (ka != kb) return ka > kb;
-    if (a.sym != b.sym) return a.sym < b.sym;
-    return a.param < b.param;
-}
 
 std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
@@ -650,6 +646,33 @@ void run_batch_impl(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* o
     pr.total_ms = ms_between(t_start, t_end);
     e->prof = pr;
 }
+
+}  // namespace
+
+// Device sources of the multi-GPU exchange (comm.cpp): the last run's top-k (header record +
+// records) and trade counter, on the engine's top-k stream after the run's top-k chain.
+bool bt::engine_exchange_view(bt_engine* e, ExchangeView& v, std::string& err) {
+    if (!e || !e->ran || e->cfg.topk <= 0 || !e->d_top.p) {
+        err = "exchange needs an engine with topk > 0 and a finished bt_run";
+        return false;
+    }
+    v.tstream = e->tstream;
+    v.device = e->cfg.device;
+    v.topk = e->cfg.topk;
+    v.d_top = e->d_top.p;
+    v.d_ntr = e->d_ntr[e->cur].p;
+    v.bar_evals = 0;
+    for (const SymDesc& s : e->syms) v.bar_evals += (int64_t)s.bars * e->P;
+    return true;
+}
+
+// The exchange's copies out of the run's buffers were enqueued on tstream: the next run that
+// reuses those buffers waits for them (same bookkeeping as bt_topk_fetch_async).
+void bt::engine_exchange_enqueued(bt_engine* e) {
+    if (hipEventRecord(e->ev_tdone[e->cur], e->tstream) == hipSuccess) e->tdone_armed[e->cur] = true;
+}
+
+namespace {
 
 #define ABI_GUARD(fail, ...)                                   \
     try {                                                      \

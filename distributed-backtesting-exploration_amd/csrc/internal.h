@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/bt.h"
 
 // Profiling switches (phase ablation, s_memtime stamps, launch-shape overrides from the
@@ -92,6 +94,19 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
                        int64_t n, int32_t P, int32_t k, const TopkWork& w, hipStream_t st);
 hipError_t launch_topk_init(const TopkWork& w, hipStream_t st);  // once per buffer allocation
 
+// Host-side pieces shared by engine.cpp and comm.cpp.
+void set_last_error(const std::string& s);  // bt_last_error() of this thread
+inline bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b);  // "a ranks before b"
+struct ExchangeView {
+    hipStream_t tstream;
+    int32_t device, topk;
+    const bt_topk_rec* d_top;            // [0] = header (record count), then topk records
+    const unsigned long long* d_ntr;     // trades of the last run
+    int64_t bar_evals;
+};
+bool engine_exchange_view(bt_engine* e, ExchangeView& v, std::string& err);
+void engine_exchange_enqueued(bt_engine* e);
+
 // Shared host/device helpers.
 __host__ __device__ inline uint64_t order_key(double x) {
     union { double d; uint64_t u; } v;
@@ -138,6 +153,13 @@ __host__ __device__ inline double i128_to_double(uint64_t lo, int64_t hi) {
     r = __builtin_ldexp(r, 75 - lz);
 #endif
     return neg ? -r : r;
+}
+
+inline bool topk_less(const bt_topk_rec& a, const bt_topk_rec& b) {
+    const uint64_t ka = order_key(a.sharpe), kb = order_key(b.sharpe);
+    if (ka != kb) return ka > kb;
+    if (a.sym != b.sym) return a.sym < b.sym;
+    return a.param < b.param;
 }
 
 __host__ __device__ inline double sharpe_fx(uint64_t s1lo, int64_t s1hi, uint64_t s2lo,

@@ -132,6 +132,13 @@ def lib():
     L.bt_encode_columns.restype = C.c_int64
     L.bt_gen_payload.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, P, C.c_size_t]
     L.bt_gen_payload.restype = C.c_int64
+    L.bt_comm_unique_id.argtypes = [P]
+    L.bt_comm_create.argtypes = [P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_size_t]
+    L.bt_comm_create.restype = P
+    L.bt_comm_destroy.argtypes = [P]
+    L.bt_comm_destroy.restype = None
+    L.bt_exchange_async.argtypes = [P, P, C.c_int32]
+    L.bt_exchange_wait.argtypes = [P, C.c_int32, P, C.c_int32, P]
     L.bt_last_batch_profile.argtypes = [P, C.POINTER(_BatchProfile)]
     L.bt_format_summaries.argtypes = [P, C.c_int32, P, C.c_size_t]
     L.bt_format_summaries.restype = C.c_int64
@@ -375,6 +382,47 @@ class Engine:
         pr = _BatchProfile()
         _check(lib().bt_last_batch_profile(self._h, C.byref(pr)))
         return {f: getattr(pr, f) for f, _ in _BatchProfile._fields_}
+
+
+class Comm:
+    """The multi-GPU exchange behind the C ABI (bt_comm_*, csrc/comm.cpp): one RCCL all-gather
+    per run of every rank's top-k records and counters, from the engine's device buffers."""
+
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(Comm.ID_BYTES)
+        _check(lib().bt_comm_unique_id(buf))
+        return buf.raw
+
+    def __init__(self, uid: bytes, rank: int, world: int, device: int, k: int):
+        if len(uid) != Comm.ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        err = C.create_string_buffer(512)
+        self._uid = C.create_string_buffer(bytes(uid), Comm.ID_BYTES)
+        h = lib().bt_comm_create(self._uid, rank, world, device, k, err, 512)
+        if not h:
+            raise BtError(err.value.decode())
+        self._h, self.k, self.world = h, k, world
+
+    def exchange_async(self, engine: "Engine", slot: int) -> None:
+        _check(lib().bt_exchange_async(self._h, engine._h, slot))
+
+    def exchange_wait(self, slot: int, k=None) -> tuple:
+        """Merged global top-k and [bar-evals, trades] summed over ranks."""
+        k = k or self.k
+        out = np.zeros(k, TOPK_DTYPE)
+        cnt = np.zeros(2, np.int64)
+        m = _check(lib().bt_exchange_wait(self._h, slot, out.ctypes.data, k, cnt.ctypes.data))
+        return out[:m], [int(cnt[0]), int(cnt[1])]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().bt_comm_destroy(self._h)
+            self._h = None
+
+    __del__ = close
 
 
 def merge_topk(records: np.ndarray, k: int) -> np.ndarray:

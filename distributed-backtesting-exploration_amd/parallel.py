@@ -68,6 +68,15 @@ def exchange(local: np.ndarray, k: int, counters, dist) -> tuple:
     return top, [int(x) for x in g[:, 3 * k + 1:].sum(axis=0)]
 
 
+def make_comm(dist, device: int, k: int):
+    """The C-ABI exchange (engine.Comm over RCCL) for this process group: rank 0 creates the RCCL
+    unique id, the launcher's process group broadcasts it, every rank joins."""
+    from .engine import Comm
+    obj = [Comm.unique_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return Comm(obj[0], dist.get_rank(), dist.get_world_size(), device, k)
+
+
 def allreduce_counters(values, dist) -> list:
     """Sum int64 run counters (bar-evals, trades, errors) over all ranks."""
     import torch

@@ -191,6 +191,26 @@ int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n);
 /* ---- top-k merge (host): merge sorted record lists from several shards (RCCL gather). */
 int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* out);
 
+/* ---- multi-GPU exchange (comm.cpp): one process per GPU, each running its own
+ * symbol shard; per run ONE RCCL all-gather over xGMI of every rank's top-k records and
+ * counters, straight from the engine's device buffers. Replaces nothing in the reference, whose
+ * only parallelism is job farming over gRPC (/root/reference/src/server/main.rs:131-143).
+ *   rank 0: bt_comm_unique_id(id); the launcher broadcasts the 128 bytes; every rank:
+ *   bt_comm_create(id, rank, world, device, k) — a collective call, all ranks together.
+ * bt_exchange_async enqueues the exchange of the engine's last run (which needs topk >= k) into
+ * pinned slot 0 or 1 behind the run's top-k chain, without a host wait; bt_exchange_wait returns
+ * the merged global top-k (count) and counters[2] = {bar-evals, trades} summed over ranks.
+ * Every rank must issue the same sequence of exchanges. */
+#define BT_COMM_ID_BYTES 128
+typedef struct bt_comm bt_comm;
+int32_t bt_comm_unique_id(uint8_t* out);
+bt_comm* bt_comm_create(const uint8_t* id, int32_t rank, int32_t world, int32_t device, int32_t k,
+                        char* err, size_t errlen);
+void bt_comm_destroy(bt_comm* c);
+int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot);
+int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
+                         int64_t* counters);
+
 /* ---- self-test hooks (host-side helpers the tests call without a GPU) */
 /* The CompleteRequest.data text of P summaries (spec §6, one JSON line per param), as
  * bt_run_batch writes it; returns its length, or the capacity needed when out is NULL. */

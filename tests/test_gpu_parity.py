@@ -433,3 +433,55 @@ def test_run_batch_binary_and_csv_mixed():
             assert j["n"] == int(orc[p]["n_trades"]) and j["pnl"] == int(orc[p]["pnl"])
             assert j["mdd"] == int(orc[p]["mdd"]) and j["exp"] == int(orc[p]["exposure"])
             assert float(j["sharpe"]) == float(orc[p]["sharpe"]) and int(j["h"], 16) == int(orc[p]["hash"])
+
+
+def test_rccl_exchange_world1_matches_local_topk():
+    """The C-ABI RCCL exchange (bt_comm_*, comm.cpp) at world size 1 on the MI355X: an
+    all-gather from the engine's device top-k, pipelined over both slots, returns that run's
+    top-k and counters exactly."""
+    grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
+    comm = E.Comm(E.Comm.unique_id(), 0, 1, 0, 20)
+    try:
+        with D.Engine(grid, topk=20) as e:
+            refs = []
+            for first in (0, 300):
+                e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
+                e.run()
+                refs.append((e.read_topk(), e.stats()))
+            e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
+            e.run()
+            comm.exchange_async(e, 0)
+            e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)
+            e.run()
+            comm.exchange_async(e, 1)
+            for slot, (top, st) in enumerate(refs):
+                got, cnt = comm.exchange_wait(slot)
+                assert got.tolist() == top.tolist()
+                assert cnt == [st["bar_evals"], st["trades"]]
+    finally:
+        comm.close()
+
+
+def test_torch_nccl_backend_exchange_world1():
+    """parallel.exchange over torch.distributed's "nccl" backend (RCCL) with device tensors, at
+    world size 1: the branch bench.py takes on multi-GPU nodes has run on an MI355X."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from dbx_amd import parallel as PAR
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        recs = np.zeros(5, D.TOPK_DTYPE)
+        recs["sharpe"] = [3.0, 2.0, 2.0, 1.0, 0.5]
+        recs["sym"] = [4, 1, 2, 9, 9]
+        recs["param"] = [0, 7, 3, 1, 2]
+        top, cnt = PAR.exchange(recs, 5, [123, 45], dist)
+        assert top.tolist() == recs.tolist() and cnt == [123, 45]
+        comm = PAR.make_comm(dist, 0, 5)
+        comm.close()
+    finally:
+        dist.destroy_process_group()
