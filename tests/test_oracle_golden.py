@@ -8,6 +8,8 @@ import json
 import os
 
 import numpy as np
+
+import dbx_amd as D
 import pytest
 
 import orc_ffi as F
@@ -89,17 +91,51 @@ def test_edge_golden(golden_dir):
                 _check_case(strategy, ohlc, case, ann, f"edge {series['name']} {strategy}")
 
 
-def test_fixed_point_sharpe_close_to_naive_fp64():
-    """Spec §3: the exact fixed-point Sharpe agrees with a naive fp64 sequential-sum Sharpe
-    far inside north_star's 1e-9 relative tolerance on well-conditioned lanes."""
-    worst = 0.0
-    for sym in range(4):
-        o, h, lo, c, v = F.gen(0x5EED, sym, 2520, 0)
-        for f, s in [(4, 50), (10, 120), (42, 240)]:
-            r, _ = F.sma(c, f, s, 252)
-            if abs(r["sharpe_f64"]) > 1e-3:
-                worst = max(worst, abs(r["sharpe"] / r["sharpe_f64"] - 1))
-    assert worst < 1e-11
+def _rel_gaps(rows):
+    fx = rows["sharpe"].astype(float)
+    nv = rows["sharpe_f64"].astype(float)
+    g = np.abs(fx - nv) / np.maximum(np.abs(nv), 1e-300)
+    g[(fx == 0) & (nv == 0)] = 0.0      # both exactly 0: no position, or zero variance
+    return g
+
+
+def test_fixed_point_sharpe_matches_fp64_definition_at_scale():
+    """north_star bounds Sharpe to 1e-9 relative against the scalar fp64 oracle; SURVEY A.3 defines
+    it with sequential fp64 sums of the per-bar returns. The spec's exact fixed-point Sharpe
+    (docs/oracle_spec.md §3, what the GPU reproduces bit-for-bit) is checked against that fp64
+    definition (the oracle's sharpe_f64) for EVERY parameter of sampled symbols of configs 2-5 at
+    full length. No lane class is excluded: lanes where both are exactly 0 (never in a position,
+    or zero return variance) compare equal, every other lane must be within 1e-9 relative.
+    Measured worst gaps are recorded in docs/oracle_spec.md §3."""
+    worst = {}
+    # config 2: 100 of 5,000 symbols x 2,520 daily bars x 400 params
+    cl = np.stack([F.gen(0x5EED, s, 2520, 0)[3] for s in range(0, 5000, 50)])
+    worst[2] = _rel_gaps(F.sma_grid_mt(cl, np.arange(4, 43, 2), np.arange(50, 241, 10), 252, 8).reshape(-1))
+    # config 5: first and last symbol of the 10,000 x 491,400 1-min bars x 1,024 params
+    cl = np.stack([F.gen(0x5EED, s, 491400, 1)[3] for s in (0, 9999)])
+    worst[5] = _rel_gaps(F.sma_grid_mt(cl, np.arange(5, 161, 5), np.arange(200, 6401, 200), 98280, 8).reshape(-1))
+    # config 3: 3 of 500 symbols x 98,280 bars x 64 params
+    g3 = D.config3_grid()
+    rows = []
+    for s in (0, 250, 499):
+        c = F.gen(0x5EED, s, 98280, 1)[3]
+        for p in range(g3.n_params):
+            kw = g3.param(p)
+            rows.append(F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], 98280)[0])
+    worst[3] = _rel_gaps(np.array(rows))
+    # config 4: 2 of 2,000 symbols x 98,280 bars x 256 params
+    g4 = D.config4_grid()
+    rows = []
+    for s in (0, 1999):
+        o, h, lo, c, v = F.gen(0x5EED, s, 98280, 1)
+        for p in range(g4.n_params):
+            kw = g4.param(p)
+            rows.append(F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], 98280)[0])
+    worst[4] = _rel_gaps(np.array(rows))
+    report = {k: (len(v), float(v.max())) for k, v in worst.items()}
+    print("lanes and worst relative gap per config:", report)
+    for k, (n, w) in report.items():
+        assert n > 0 and w <= 1e-9, (k, w)
 
 
 def test_numpy_restatement_matches_c_fresh():
