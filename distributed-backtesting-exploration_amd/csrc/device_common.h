@@ -4,8 +4,12 @@
 
 namespace bt {
 
-constexpr uint64_t kFnvOff = 0xCBF29CE484222325ULL;
-constexpr uint64_t kFnvPrime = 0x100000001B3ULL;
+// Trade hash (spec §4): h = sum over trades of mix(w) mod 2^64, w = entry | exit << 31 |
+// (side > 0) << 62. A sum, so the hashes of consecutive bar segments add (k_tile.hip segments).
+__host__ __device__ inline uint64_t trade_mix(uint64_t w) {
+    const uint64_t z = (w ^ (w >> 29)) * 0xBF58476D1CE4E5B9ULL;
+    return z ^ (z >> 32);
+}
 constexpr int kDstLevels = 6;      // log2(kTile)
 constexpr int kKeyStride = kTile + 1;  // +1 double per key row: conflict-free ds_read_b64
 

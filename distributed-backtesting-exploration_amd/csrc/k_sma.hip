@@ -255,7 +255,7 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int
     a.R += pnl;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)lg << 62);
-    a.h = (a.h ^ w) * kFnvPrime;
+    a.h += trade_mix(w);
     if (PARITY && a.ntr < cap) {
         bt_trade r;
         r.entry_bar = a.e;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     a.pos = a.e = a.ce = a.sb = a.ntr = a.e0 = 0;
     a.R = a.gap = a.mdd = 0;
     a.ps1 = a.ps2 = 0;
-    a.h = kFnvOff;
+    a.h = 0;
     a.s1 = a.s2 = 0;
     a.agg = kAggId;
     bt_trade* tr = nullptr;

@@ -74,7 +74,7 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
     a.pos = a.e = a.ce = a.sb = a.ntr = a.expo = 0;
     a.R = a.gap = a.mdd = 0;
     a.ps1 = a.ps2 = 0;
-    a.h = kFnvOff;
+    a.h = 0;
     a.s1 = a.s2 = 0;
     a.agg = kAggId;
 }
@@ -95,7 +95,7 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, cons
     a.expo += t - a.e;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)lg << 62);
-    a.h = (a.h ^ w) * kFnvPrime;
+    a.h += trade_mix(w);
     if (PARITY && a.ntr < cap) {
         bt_trade r;
         r.entry_bar = a.e;

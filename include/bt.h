@@ -93,7 +93,7 @@ typedef struct bt_summary {
     int64_t mdd;                      /* ticks */
     int64_t exposure;                 /* bars held */
     double sharpe;
-    uint64_t hash;                    /* FNV-1a trade-sequence hash (spec §4) */
+    uint64_t hash;                    /* additive trade-sequence hash (spec §4) */
 } bt_summary;
 
 typedef struct bt_trade {

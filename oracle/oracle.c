@@ -21,8 +21,12 @@
 
 #define GOLDEN 0x9E3779B97F4A7C15ULL
 #define TWO56 72057594037927936.0
-#define FNV_OFF 0xCBF29CE484222325ULL
-#define FNV_PRIME 0x100000001B3ULL
+/* trade hash (spec §4): h = sum of mix(w) over trades, mod 2^64 */
+#define MIX_K 0xBF58476D1CE4E5B9ULL
+static uint64_t trade_mix(uint64_t w) {
+    uint64_t z = (w ^ (w >> 29)) * MIX_K;
+    return z ^ (z >> 32);
+}
 
 /* ---------------------------------------------------------------- A.1 generator */
 static uint64_t draw(uint64_t s0, uint64_t k) {
@@ -240,7 +244,7 @@ typedef struct acct {
 
 static void acct_init(acct* a, orc_trade* tr, int32_t cap) {
     memset(a, 0, sizeof(*a));
-    a->hash = FNV_OFF;
+    a->hash = 0;
     a->tr = tr;
     a->cap = cap;
 }
@@ -264,7 +268,7 @@ static void acct_close(acct* a, int32_t t, int64_t px) {
     a->R += a->pos * (px - a->entry_px);
     const uint64_t w = (uint64_t)(uint32_t)a->entry_bar | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)(a->pos > 0) << 62);
-    a->hash = (a->hash ^ w) * FNV_PRIME;
+    a->hash += trade_mix(w);
     if (a->tr && a->ntr < a->cap) {
         orc_trade* r = &a->tr[a->ntr];
         r->entry_bar = a->entry_bar;

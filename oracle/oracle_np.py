@@ -19,8 +19,7 @@ import numpy as np
 
 GOLDEN = 0x9E3779B97F4A7C15
 MASK = (1 << 64) - 1
-FNV_OFF = 0xCBF29CE484222325
-FNV_PRIME = 0x100000001B3
+MIX_K = 0xBF58476D1CE4E5B9  # trade hash (spec §4): h = sum of mix(w) mod 2^64
 DAILY, MINUTE = 0, 1
 
 
@@ -125,7 +124,7 @@ def account(c, positions, exits, ann):
     entry_bar = entry_px = 0
     realized = peak = mdd = 0
     s1 = s2 = expo = 0
-    h = FNV_OFF
+    h = 0
     for t in range(len(c)):
         if t >= 1 and pos:
             s1 += pos * q[t]
@@ -137,7 +136,8 @@ def account(c, positions, exits, ann):
                 px = exits[t] if exits[t] is not None else int(c[t])
                 realized += pos * (px - entry_px)
                 w = entry_bar | (t << 31) | ((1 if pos > 0 else 0) << 62)
-                h = ((h ^ w) * FNV_PRIME) & MASK
+                z = ((w ^ (w >> 29)) * MIX_K) & MASK
+                h = (h + (z ^ (z >> 32))) & MASK
                 trades.append((entry_bar, t, pos, entry_px, px))
             if np_:
                 entry_bar, entry_px = t, int(c[t])
