@@ -94,6 +94,11 @@ struct bt_engine {
     int64_t nrun = 0;
     DevBuf<bt_sums> d_sums;
     DevBuf<bt_trade> d_trades;
+    // Bollinger bar segments (k_tile.hip): requested count (0 = auto, 1 = off), burn-in tiles,
+    // the records of a split run and the count the last run used
+    int32_t seg_req = 0, seg_burn = kDefaultBurnTiles, seg_last = 1;
+    DevBuf<SegRec> d_seg;
+    DevBuf<unsigned long long> d_refixed;
     DevBuf<unsigned long long> d_dbg;
     // top-k chain stream: the chain of run i overlaps the kernel of run i+1
     hipStream_t tstream = nullptr;
@@ -349,10 +354,25 @@ void run_impl(bt_engine* e) {
         case BT_EMA_OLS:
             err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
             break;
-        case BT_BOLL:
+        case BT_BOLL: {
+            SegArgs sg{nullptr, nullptr, 1, e->seg_burn};
+            if (!parity) {
+                int32_t maxb = 0;
+                for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);
+                sg.G = e->seg_req > 0 ? e->seg_req : boll_auto_segments(S, e->P, maxb);
+            }
+            if (sg.G > 1) {
+                e->d_seg.ensure((size_t)sg.G * S * e->P);
+                e->d_refixed.ensure(1);
+                HIPCHK(hipMemsetAsync(e->d_refixed.p, 0, sizeof(unsigned long long), e->stream));
+                sg.rec = e->d_seg.p;
+                sg.refixed = e->d_refixed.p;
+            }
+            e->seg_last = sg.G;
             err = launch_boll(e->d_syms.p, S, e->d_h.p, e->d_l.p, e->d_c.p, e->grid, out, parity,
-                              e->stream);
+                              sg, e->stream);
             break;
+        }
     }
     HIPCHK(err);
     if (timing) {
@@ -774,6 +794,8 @@ void bt_engine_destroy(bt_engine* e) {
         e->ev_kdone = nullptr;
         e->d_sums.release();
         e->d_trades.release();
+        e->d_seg.release();
+        e->d_refixed.release();
         e->d_dbg.release();
         e->d_hist.release();
         e->d_counts.release();
@@ -805,6 +827,31 @@ void bt_engine_destroy(bt_engine* e) {
 }
 
 int32_t bt_num_params(const bt_engine* e) { return e ? e->P : -1; }
+
+int32_t bt_set_segments(bt_engine* e, int32_t segments, int32_t burn_tiles) {
+    ABI_GUARD(-1, {
+        if (!e || segments < 0 || segments > 64 || burn_tiles < 0) throw HipFail{"bad arguments"};
+        e->seg_req = segments;
+        e->seg_burn = burn_tiles > 0 ? burn_tiles : kDefaultBurnTiles;
+        return 0;
+    })
+}
+
+int32_t bt_last_segments(bt_engine* e, int64_t* refixed_blocks) {
+    ABI_GUARD(-1, {
+        if (!e) throw HipFail{"null engine"};
+        if (refixed_blocks) {
+            unsigned long long n = 0;
+            if (e->seg_last > 1 && e->d_refixed.p) {
+                activate(e);
+                sync_all(e);
+                HIPCHK(hipMemcpy(&n, e->d_refixed.p, sizeof n, hipMemcpyDeviceToHost));
+            }
+            *refixed_blocks = (int64_t)n;
+        }
+        return e->seg_last;
+    })
+}
 
 int32_t bt_load_synthetic(bt_engine* e, uint64_t seed, int64_t sym_begin, int32_t n_sym,
                           int32_t n_bars, int32_t freq) {

@@ -73,9 +73,40 @@ size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
 size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, hipStream_t st);
+// Bar-axis split of the Bollinger walk (k_tile.hip): each symbol's tiles are cut into G
+// segments walked by separate workgroups. Segment s >= 1 starts flat `burn_tiles` tiles before
+// its first bar (a walk whose accounting is discarded) and records the state it reached there;
+// a fix pass per boundary re-walks a segment from the true state (the previous segment's end)
+// if any lane's state differs, and a combine pass folds the segments' additive sums and
+// max-plus drawdown forms into the summaries. One record per (segment, symbol, param), in
+// result param order: rec[(s * n_sym + sym) * P + p].
+struct SegRec {
+    int32_t ntr, expo;
+    int32_t start_pos, start_e;    // state at the segment's first accounted bar
+    int32_t end_pos, end_e, end_ce, pad;
+    int32_t end_agg[4];            // Agg of the open trade's path at the segment end
+    int64_t R;                     // realized pnl of trades closed in the segment
+    int64_t A, B, C, D;            // drawdown as functions of the entering gap g and mdd m:
+                                   // gap' = max(g + A, B), mdd' = max(m, g + C, D)
+    uint64_t h;                    // additive trade hash
+    uint64_t s1lo;
+    int64_t s1hi;
+    uint64_t s2lo;
+    int64_t s2hi;
+};
+static_assert(sizeof(SegRec) == 128, "SegRec layout");
+struct SegArgs {
+    SegRec* rec;
+    unsigned long long* refixed;   // fix-pass blocks that re-walked their segment
+    int32_t G;                     // segments per symbol (1 = no split)
+    int32_t burn_tiles;            // tiles walked before a speculative segment's first bar
+};
+constexpr int kDefaultBurnTiles = 64;
 hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, const int32_t* low,
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
-                       hipStream_t st);
+                       const SegArgs& seg, hipStream_t st);
+// Segments per symbol the Bollinger launcher would choose for this shard (auto mode).
+int32_t boll_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars);
 
 // Top-k by radix select over `key` (k_topk.hip): device-side finish into `out`.
 constexpr int kTopkCap = 2048;      // candidates sorted in LDS by the finish kernel

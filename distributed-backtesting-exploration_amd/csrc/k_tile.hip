@@ -423,12 +423,17 @@ __device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t 
 // (tests/test_oracle_golden.py::test_sltp_level_floor checks every f against integer division).
 __device__ __forceinline__ double level_y(double ce, double g) { return ce * g + 0x1p-16; }
 
-template <bool PARITY, bool STAMPS>
+// SEG: one bar segment per block (blockIdx.z = segment; or, with fix_seg >= 1, the fix pass of
+// boundary fix_seg: the block re-walks that segment from the previous segment's end states if
+// any lane's speculative start differs, and otherwise returns at once). Results go to SegRec
+// records (internal.h) that boll_seg_combine folds.
+template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
                                                          const int32_t* __restrict__ high,
                                                          const int32_t* __restrict__ low,
                                                          const int32_t* __restrict__ close,
-                                                         Grid g, Out out, int nextra, int lpw) {
+                                                         Grid g, Out out, int nextra, int lpw,
+                                                         SegArgs sg, int fix_seg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(1, R, nw, nk);
@@ -472,16 +477,46 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int64_t kd2 = (int64_t)g.k_den * g.k_den;
     const double kd2d = (double)kd2;
 
+    // tiles of this block: scanned from T_scan (every window of the first walked bar complete),
+    // walked from T_walk, accounted from T_acct, up to T_end (exclusive)
+    int T_scan = 0, T_walk = 0, T_acct = 0, T_end = ntiles, seg = 0;
+    const SegRec* prev = nullptr;
+    SegRec* mine = nullptr;
+    if (SEG) {
+        seg = fix_seg > 0 ? fix_seg : (int)blockIdx.z;
+        T_acct = (int)((int64_t)seg * ntiles / sg.G);
+        T_end = (int)((int64_t)(seg + 1) * ntiles / sg.G);
+        T_walk = (fix_seg > 0 || seg == 0) ? T_acct : max(0, T_acct - sg.burn_tiles);
+        T_scan = max(0, T_walk - (g.wmax - 1 + kTile - 1) / kTile);
+        if (T_acct >= T_end) T_scan = T_walk = T_acct = T_end;  // empty segment: state passes through
+        const size_t per_seg = (size_t)gridDim.x * P;
+        mine = sg.rec + seg * per_seg + (size_t)blockIdx.x * P + pj;
+        if (seg > 0) prev = mine - per_seg;
+        if (fix_seg > 0) {
+            // the fix pass re-walks only if some lane's speculative start state is not the true one
+            bool differs = false;
+            if (active) {
+                const int tp = prev->end_pos, te = prev->end_e;
+                differs = !(mine->start_pos == tp && (tp == 0 || mine->start_e == te));
+            }
+            if (!__syncthreads_or(differs)) return;
+            if (tid == 0) atomicAdd(sg.refixed, 1ULL);
+        }
+    }
+
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
     for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
     if (tid == 0) {
-        r1[0] = 0;
-        r2[0] = 0;
-        *ctr = 0;
+        // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
+        r1[(T_scan * kTile) % R] = 0;
+        r2[(T_scan * kTile) % R] = 0;
+        // task rounds are numbered by tile (flags): the counter starts at round T_scan
+        const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
+        *ctr = (uint32_t)T_scan * (uint32_t)(nw + ngrab0);
     }
     __syncthreads();
 
-    TileCarry cy{0, 0};
+    TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     unsigned __int128 cy2 = 0;
     int32_t cpre = 0, hpre = 0, lpre = 0;
 
@@ -591,34 +626,55 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     };
 
     if (helper) {
-        const int32_t c0 = ldc(crow, B, lane, 0), c1 = ldc(crow, B, kTile + lane, 0);
-        const int32_t h0 = ldc(hrow, B, lane, 0), h1 = ldc(hrow, B, kTile + lane, 0);
-        const int32_t l0 = ldc(lrow, B, lane, INT32_MAX), l1 = ldc(lrow, B, kTile + lane, INT32_MAX);
-        cpre = ldc(crow, B, 2 * kTile + lane, 0);
-        hpre = ldc(hrow, B, 2 * kTile + lane, 0);
-        lpre = ldc(lrow, B, 2 * kTile + lane, INT32_MAX);
-        scan(0, c0, h0, l0);
+        const int b0 = T_scan * kTile;
+        const int32_t c0 = ldc(crow, B, b0 + lane, 0), c1 = ldc(crow, B, b0 + kTile + lane, 0);
+        const int32_t h0 = ldc(hrow, B, b0 + lane, 0), h1 = ldc(hrow, B, b0 + kTile + lane, 0);
+        const int32_t l0 = ldc(lrow, B, b0 + lane, INT32_MAX), l1 = ldc(lrow, B, b0 + kTile + lane, INT32_MAX);
+        cpre = ldc(crow, B, b0 + 2 * kTile + lane, 0);
+        hpre = ldc(hrow, B, b0 + 2 * kTile + lane, 0);
+        lpre = ldc(lrow, B, b0 + 2 * kTile + lane, INT32_MAX);
+        if (T_scan < T_end) scan(T_scan, c0, h0, l0);
         __syncthreads();
-        if (ntiles > 1) scan(1, c1, h1, l1);
+        if (T_scan + 1 < T_end) scan(T_scan + 1, c1, h1, l1);
     } else {
         __syncthreads();
     }
-    flags(0);
+    if (T_scan < T_end) flags(T_scan);
     __syncthreads();
 
     TradeAcct a;
     acct_init(a);
     // open trade: lows <= XL hit the low-side level, highs > XHm1 the high-side level
     int32_t XL = 0, XHm1 = 0;
+    // low-side level: long SL / short TP (< ce); high-side: long TP / short SL (may reach 2^31:
+    // no high can exceed it then)
+    auto set_levels = [&](int32_t cx, int np) {
+        const double cd = (double)cx;
+        const double yl = level_y(cd, np > 0 ? gl_long : gl_short);
+        const double yh = level_y(cd, np > 0 ? gh_long : gh_short);
+        XL = (int32_t)yl;
+        XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
+    };
+    int32_t start_pos = 0, start_e = 0;  // SEG: state at the first accounted bar
+    if (SEG && fix_seg > 0 && active) {  // the true state entering the segment
+        a.pos = prev->end_pos;
+        a.e = prev->end_e;
+        a.ce = prev->end_ce;
+        a.agg = Agg{prev->end_agg[0], prev->end_agg[1], prev->end_agg[2], prev->end_agg[3]};
+        a.sb = 0;
+        if (a.pos != 0) set_levels(a.ce, a.pos);
+        start_pos = a.pos;
+        start_e = a.e;
+    }
     const size_t gi = (size_t)blockIdx.x * P + pj;
     bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
 
     StampAcc sa;
     if (STAMPS) sa.begin();
-    for (int k = 0; k < ntiles; ++k) {
+    for (int k = T_scan; k < T_end; ++k) {
         const int t0 = k * kTile;
-        if (helper && k + 2 < ntiles) {
+        if (helper && k + 2 < T_end) {
             scan(k + 2, cpre, hpre, lpre);
             const int tn = t0 + 3 * kTile + lane;
             cpre = ldc(crow, B, tn, 0);
@@ -626,7 +682,20 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             lpre = ldc(lrow, B, tn, INT32_MAX);
         }
         if (STAMPS) sa.mark(0);
-        if (active && !BT_ABL(g, 8)) {
+        if (SEG && k == T_acct && active) {
+            // first accounted tile: keep the state the (speculative) walk reached, drop the
+            // burn-in's sums (a trade open here is closed and accounted in this segment)
+            start_pos = a.pos;
+            start_e = a.e;
+            a.R = 0;
+            a.A = 0;
+            a.Bq = a.C = a.D = kNegInf;
+            a.ntr = a.expo = 0;
+            a.h = 0;
+            a.s1 = a.s2 = 0;
+            a.ps1 = a.ps2 = 0;
+        }
+        if (active && k >= T_walk && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
@@ -658,13 +727,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     a.ps2 -= q2x;
                     acct_open(a, t0 + b, b, cx);
                     a.pos = np;
-                    // low-side level: long SL / short TP (< ce); high-side: long TP / short SL
-                    // (may reach 2^31: no high can exceed it then)
-                    const double cd = (double)cx;
-                    const double yl = level_y(cd, np > 0 ? gl_long : gl_short);
-                    const double yh = level_y(cd, np > 0 ? gh_long : gh_short);
-                    XL = (int32_t)yl;
-                    XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
+                    set_levels(cx, np);
                     cur = b + 1;
                 }
                 if (cur >= kTile) return false;
@@ -690,7 +753,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
                 const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                acct_close<PARITY>(a, t0 + x, px, st, tr, cap);
+                acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
                 a.ps1 += lg ? qx : (uint64_t)0 - qx;
                 a.ps2 += q2x;
                 a.pos = 0;
@@ -706,14 +769,85 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !BT_ABL(g, 2)) flags(k + 1);
+        if (k + 1 < T_end && !BT_ABL(g, 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
     }
     if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helper ? 1 : 3), lane);
+    if (SEG) {
+        if (active) {
+            SegRec r;
+            r.ntr = a.ntr;
+            r.expo = a.expo;
+            r.start_pos = start_pos;
+            r.start_e = start_e;
+            r.end_pos = a.pos;
+            r.end_e = a.e;
+            r.end_ce = a.ce;
+            r.pad = 0;
+            r.end_agg[0] = a.agg.mx;
+            r.end_agg[1] = a.agg.mn;
+            r.end_agg[2] = a.agg.dd;
+            r.end_agg[3] = a.agg.du;
+            r.R = a.R;
+            r.A = a.A;
+            r.B = a.Bq;
+            r.C = a.C;
+            r.D = a.D;
+            r.h = a.h;
+            r.s1lo = (uint64_t)a.s1;
+            r.s1hi = (int64_t)(a.s1 >> 64);
+            r.s2lo = (uint64_t)a.s2;
+            r.s2hi = (int64_t)(a.s2 >> 64);
+            *mine = r;
+        }
+        return;
+    }
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
     wave_add_trades(out, active ? a.ntr : 0);
+}
+
+// Folds the bar segments of every (symbol, param) in order: additive counts, pnl, hash and
+// return sums; the drawdown forms composed from g = m = 0 (tile_common.h TradeAcct).
+__global__ __launch_bounds__(256) void boll_seg_combine(const SymDesc* __restrict__ syms,
+                                                        int n_sym, int P, const SegRec* __restrict__ rec,
+                                                        int G, double sqrt_ann, Out out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t n = (size_t)n_sym * P;
+    int ntr = 0;
+    if (i < n) {
+        const int s = (int)(i / P);
+        int64_t expo = 0, R = 0, gap = 0, mdd = 0;
+        uint64_t h = 0;
+        i128 s1 = 0, s2 = 0;
+        for (int q = 0; q < G; ++q) {
+            const SegRec& r = rec[(size_t)q * n + i];
+            ntr += r.ntr;
+            expo += r.expo;
+            R += r.R;
+            h += r.h;
+            s1 += (i128)(((unsigned __int128)(uint64_t)r.s1hi << 64) | r.s1lo);
+            s2 += (i128)(((unsigned __int128)(uint64_t)r.s2hi << 64) | r.s2lo);
+            mdd = max(mdd, max(gap + r.C, r.D));
+            gap = max(gap + r.A, r.B);
+        }
+        const uint64_t s1lo = (uint64_t)s1, s2lo = (uint64_t)s2;
+        const int64_t s1hi = (int64_t)(s1 >> 64), s2hi = (int64_t)(s2 >> 64);
+        const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, syms[s].bars, sqrt_ann);
+        bt_summary r;
+        r.n_trades = ntr;
+        r.status = 0;
+        r.pnl = R;
+        r.mdd = mdd;
+        r.exposure = expo;
+        r.sharpe = sh;
+        r.hash = h;
+        out.sum[i] = r;
+        out.key[i] = order_key(sh);
+        if (out.sums != nullptr) out.sums[i] = bt_sums{s1lo, s1hi, s2lo, s2hi};
+    }
+    wave_add_trades(out, ntr);
 }
 
 // ----------------------------------------------------------------------------- launchers
@@ -784,30 +918,56 @@ hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* clo
     return hipGetLastError();
 }
 
+// Bar segments per symbol for a shard of n_sym symbols: a shard with no more blocks than CUs
+// leaves every CU one latency-bound block (config 4 on 8 GPUs: 250 symbols, 7.95 ms), so its
+// series are cut into up to 4 segments, enough for two blocks per CU, each segment at least
+// twice the burn-in long.
+int32_t boll_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars) {
+    if (n_sym <= 0) return 1;
+    const int pw = std::min((n_params + 63) / 64, 1024 / 64 - 1);
+    const long long blocks = (long long)n_sym * ((n_params + 64 * pw - 1) / (64 * pw));
+    if (blocks > device_cus()) return 1;
+    int G = (int)std::min<long long>(4, std::max<long long>(1, 2LL * device_cus() / blocks));
+    const int ntiles = (max_bars + kTile - 1) / kTile;
+    while (G > 1 && ntiles / G < 2 * kDefaultBurnTiles) --G;
+    return G;
+}
+
 hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, const int32_t* low,
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
-                       hipStream_t st) {
+                       const SegArgs& seg, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
     const int lpw = tile_lanes_per_wave();
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 1);
-    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
+    const bool split = seg.G > 1 && !parity;
+    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw), split ? seg.G : 1);
     // at most one block per CU (config 4 on 8 GPUs: 250 symbols) leaves wave slots free: four
     // task-only waves (8.17 -> 7.90 ms vs two); otherwise as many as keep the block at 8 waves,
     // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms)
-    const bool sparse = (long long)grid.x * grid.y <= device_cus();
+    const bool sparse = (long long)grid.x * grid.y * grid.z <= device_cus();
     const int xw = tile_extra_waves(pw + 1, sparse ? 4 : std::max(2, std::min(3, 8 - (pw + 1))));
     const dim3 block(64 * (pw + 1 + xw));
     const size_t lds = boll_lds_bytes(g);
 #ifdef BT_PROFILING
     if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((boll_tile_kernel<false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
+        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
         return hipGetLastError();
     }
 #endif
-    if (parity)
-        hipLaunchKernelGGL((boll_tile_kernel<true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
-    else
-        hipLaunchKernelGGL((boll_tile_kernel<false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw);
+    if (split) {
+        // speculative segments, then the fix pass of each boundary in order (a block returns at
+        // once when its lanes' starts were right), then the fold
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+        const dim3 fgrid(grid.x, grid.y, 1);
+        for (int s = 1; s < seg.G; ++s)
+            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s);
+        const size_t n = (size_t)n_sym * g.n_params;
+        hipLaunchKernelGGL(boll_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
+    } else if (parity) {
+        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+    } else {
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+    }
     return hipGetLastError();
 }
 

@@ -62,9 +62,15 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
 //    2^64, folded into int128 at the tile end): a position change at bar b from pos to np adds
 //    (pos - np) * QL[b] to ps1 and (|pos| - |np|) * QL2[b] to ps2; an open position at the tile
 //    end adds pos * QL[63] and QL2[63].
+//  * bar segments (SEG): the entering gap g and mdd m are unknown, so the drawdown is kept as
+//    gap = max(g + A, Bq), mdd = max(m, g + C, D): a trade (lo, hi, path, pnl) maps
+//    C' = max(C, A - lo), D' = max(D, Bq - lo, path), A' = A - pnl, Bq' = max(Bq, hi) - pnl.
+constexpr int64_t kNegInf = -(1LL << 60);  // "minus infinity" of the max-plus forms
+
 struct TradeAcct {
     int32_t pos, e, ce, sb, ntr, expo;  // sb: in-tile bar where the open trade's path resumes
     int64_t R, gap, mdd;
+    int64_t A, Bq, C, D;                // SEG walks only
     uint64_t ps1, ps2, h;
     i128 s1, s2;
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
@@ -73,6 +79,8 @@ struct TradeAcct {
 __device__ __forceinline__ void acct_init(TradeAcct& a) {
     a.pos = a.e = a.ce = a.sb = a.ntr = a.expo = 0;
     a.R = a.gap = a.mdd = 0;
+    a.A = 0;
+    a.Bq = a.C = a.D = kNegInf;
     a.ps1 = a.ps2 = 0;
     a.h = 0;
     a.s1 = a.s2 = 0;
@@ -81,7 +89,7 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
 
 // Close the open trade at global bar t for price px; `st` aggregates the trade's whole price
 // path in order, exit point included.
-template <bool PARITY>
+template <bool PARITY, bool SEG = false>
 __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
                                            bt_trade* tr, int cap) {
     const bool lg = a.pos > 0;
@@ -89,8 +97,16 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, cons
     const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
     const int32_t path = lg ? st.dd : st.du;
     const int32_t pnl = lg ? px - a.ce : a.ce - px;
-    a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
-    a.gap = max(a.gap, (int64_t)hi) - pnl;
+    if (SEG) {
+        const int64_t A0 = a.A, B0 = a.Bq;
+        a.C = max(a.C, A0 - (int64_t)lo);
+        a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
+        a.A = A0 - pnl;
+        a.Bq = max(B0, (int64_t)hi) - pnl;
+    } else {
+        a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+        a.gap = max(a.gap, (int64_t)hi) - pnl;
+    }
     a.R += pnl;
     a.expo += t - a.e;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |

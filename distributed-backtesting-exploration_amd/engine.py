@@ -105,6 +105,8 @@ def lib():
     L.bt_last_error.restype = C.c_char_p
     L.bt_abi_version.restype = C.c_int32
     L.bt_num_params.argtypes = [P]
+    L.bt_set_segments.argtypes = [P, C.c_int32, C.c_int32]
+    L.bt_last_segments.argtypes = [P, C.POINTER(C.c_int64)]
     L.bt_run_batch.argtypes = [P, C.c_size_t, C.POINTER(_JobIn), C.POINTER(_JobOut)]
     L.bt_job_out_free.argtypes = [C.POINTER(_JobOut), C.c_size_t]
     L.bt_job_out_free.restype = None
@@ -297,6 +299,16 @@ class Engine:
 
     def run(self):
         _check(lib().bt_run(self._h))
+
+    def set_segments(self, segments: int, burn_tiles: int = 0) -> None:
+        """Bollinger bar-axis split: 0 = automatic, 1 = off, n = n segments per symbol."""
+        _check(lib().bt_set_segments(self._h, segments, burn_tiles))
+
+    def last_segments(self, with_refixed: bool = False):
+        """Segments per symbol of the last run (and, with_refixed, the fix pass's re-walks)."""
+        n = C.c_int64(0)
+        g = _check(lib().bt_last_segments(self._h, C.byref(n)))
+        return (g, int(n.value)) if with_refixed else g
 
     def sync(self):
         _check(lib().bt_sync(self._h))

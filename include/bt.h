@@ -131,6 +131,15 @@ void bt_engine_destroy(bt_engine* e);
 const char* bt_last_error(void);      /* thread-local message of the last failed call */
 int32_t bt_abi_version(void);
 int32_t bt_num_params(const bt_engine* e);
+/* Bar-axis split of the Bollinger walk (k_tile.hip; small shards): segments per symbol
+ * (0 = automatic: split when the shard has no more workgroups than the GPU has CUs; 1 = never;
+ * n = always n) and the burn-in tiles a speculative segment walks before its first bar (0 = the
+ * default 64). Results are identical either way (a boundary whose speculative start differs from
+ * the true one is re-walked); parity mode (trade lists) never splits. bt_last_segments: the count
+ * the last bt_run used and, if refixed_blocks is not NULL, how many (symbol, boundary) blocks the
+ * fix pass re-walked (waits for the run). */
+int32_t bt_set_segments(bt_engine* e, int32_t segments, int32_t burn_tiles);
+int32_t bt_last_segments(bt_engine* e, int64_t* refixed_blocks);
 
 /* Phase times of the last bt_run_batch call (host clocks for host phases, HIP events for the
  * device ones). */

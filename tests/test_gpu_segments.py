@@ -1,0 +1,92 @@
+"""Bar-axis split of the Bollinger walk (k_tile.hip SEG; include/bt.h bt_set_segments): every
+summary field of a split run must equal the unsplit run and the C oracle bit for bit, whatever
+the segment count and burn-in — including burn-ins too short for the speculative walk to meet
+the true one (the fix pass re-walks those boundaries) and segments with no bars at all."""
+import numpy as np
+import pytest
+
+import dbx_amd as D
+import orc_ffi as F
+from helpers import compare_summary, oracle_row
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(grid, sym0, n_sym, bars, segments, burn=0):
+    with D.Engine(grid) as e:
+        e.set_segments(segments, burn)
+        e.load_synthetic(0x5EED, sym0, n_sym, bars, D.BT_MINUTE)
+        e.run()
+        got = e.summaries().copy()
+        used, refixed = e.last_segments(with_refixed=True)
+        st = e.stats()
+    _run.refixed = refixed
+    return got, used, st
+
+
+@pytest.mark.parametrize("segments,burn", [(2, 64), (2, 1), (3, 2), (4, 1), (5, 3)])
+def test_split_equals_unsplit_and_oracle(segments, burn):
+    grid = D.Grid.boll([10, 45, 240], [3, 5], [50, 100], [100, 400], k_den=2)
+    bars = 20000
+    ref, used1, st1 = _run(grid, 0, 3, bars, 1)
+    got, used, st = _run(grid, 0, 3, bars, segments, burn)
+    assert used1 == 1 and used == segments
+    if burn <= 2:  # one or two tiles of burn-in rarely reach the true state: the fix pass ran
+        assert _run.refixed > 0
+    assert got.tobytes() == ref.tobytes(), "split run differs from the unsplit run"
+    assert st["trades"] == st1["trades"] == int(ref["n_trades"].sum())
+    for s in range(3):
+        o, h, lo, c = F.gen(0x5EED, s, bars, 1)[:4]
+        orc, _ = oracle_row("boll", grid, (o, h, lo, c), 98280)
+        for p in range(grid.n_params):
+            compare_summary(got[s, p], orc[p], f"G={segments} burn={burn} sym {s} {grid.param(p)}")
+
+
+def test_split_config4_grid_short_burn_in():
+    """All 256 config-4 parameters, burn-in of one tile: many boundaries need the fix pass."""
+    grid = D.config4_grid()
+    ref, _, _ = _run(grid, 7, 4, 30000, 1)
+    got, used, _ = _run(grid, 7, 4, 30000, 2, 1)
+    assert used == 2 and got.tobytes() == ref.tobytes()
+
+
+def test_split_ragged_and_empty_segments():
+    """Ragged series (1 bar to a few tiles) cut into more segments than they have tiles."""
+    grid = D.Grid.boll([2, 3, 20, 70], [1, 4], [50, 100], [50, 400], k_den=2)
+    lengths = [1, 2, 63, 64, 65, 130, 700, 3000]
+    cols = [F.gen(0x5EED, 30 + i, n, 1) for i, n in enumerate(lengths)]
+    outs = []
+    for segments in (1, 4, 9):
+        with D.Engine(grid) as e:
+            e.set_segments(segments, 1)
+            e.load_ohlc([x[3] for x in cols], [x[1] for x in cols], [x[2] for x in cols])
+            e.run()
+            outs.append(e.summaries().copy())
+            assert e.last_segments() == segments
+    assert outs[1].tobytes() == outs[0].tobytes() and outs[2].tobytes() == outs[0].tobytes()
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("boll", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(grid.n_params):
+            compare_summary(outs[1][i, p], orc[p], f"ragged {lengths[i]} bars {grid.param(p)}")
+
+
+def test_auto_split_on_small_shard_matches_oracle():
+    """Automatic mode on a shard with fewer symbols than CUs (the 8-GPU config-4 shard is 250):
+    the engine splits, and sampled symbols match the oracle."""
+    grid = D.config4_grid()
+    got, used, _ = _run(grid, 100, 120, 40000, 0)
+    assert used >= 2
+    for s in (0, 77, 119):
+        o, h, lo, c = F.gen(0x5EED, 100 + s, 40000, 1)[:4]
+        orc, _ = oracle_row("boll", grid, (o, h, lo, c), 98280)
+        for p in range(0, grid.n_params, 5):
+            compare_summary(got[s, p], orc[p], f"auto split sym {100 + s} {grid.param(p)}")
+
+
+def test_parity_mode_never_splits():
+    grid = D.Grid.boll([10, 45], [3, 5], [50], [100], k_den=2)
+    with D.Engine(grid, parity=True, trade_cap=4096) as e:
+        e.set_segments(4, 1)
+        e.load_synthetic(0x5EED, 0, 2, 5000, D.BT_MINUTE)
+        e.run()
+        assert e.last_segments() == 1
