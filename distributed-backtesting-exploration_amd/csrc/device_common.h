@@ -55,6 +55,18 @@ __device__ __forceinline__ Agg dst_query_bf(const Agg* D, int a, int b) {
     return agg_merge(D[L * kTile + a], D[L * kTile + b]);
 }
 
+// dst_query_bf reading both 16-B entries whole (two ds_read_b128 in one round trip, kept live):
+// callers that need drawdown or draw-up by side then wait once instead of a second time in a
+// divergent branch.
+__device__ __forceinline__ Agg dst_query_w(const Agg* D, int a, int b) {
+    const unsigned x = (unsigned)(a ^ b);
+    const int L = x ? 31 - __builtin_clz(x) : 0;
+    const int4 u = *reinterpret_cast<const int4*>(D + L * kTile + a);
+    const int4 v = *reinterpret_cast<const int4*>(D + L * kTile + b);
+    asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    return agg_merge(Agg{u.x, u.y, u.z, u.w}, Agg{v.x, v.y, v.z, v.w});
+}
+
 // Upward-biased reciprocal for exact floor keys (k_sma.hip floor_key): RN(RN(1/W) * (1 + 2^-47)).
 __host__ __device__ inline double key_recip(int W) { return (1.0 / (double)W) * (1.0 + 0x1p-47); }
 

@@ -35,10 +35,11 @@ namespace {
 
 constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflict-free columns
 // Bollinger per-stage low/high staging (int32): lows[64], highs[64], 8 block minima of the lows
-// then 8 block maxima of the highs, and per bar the minimum low / maximum high from that bar to
-// the end of its 8-bar block (SL/TP first-passage search)
-constexpr int kLH = 4 * kTile + 16;
-constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16;
+// then 8 block maxima of the highs, per bar the minimum low / maximum high from that bar to the
+// end of its 8-bar block, and per bar the minimum low / maximum high from that bar to the end of
+// the tile (SL/TP first-passage search)
+constexpr int kLH = 6 * kTile + 16;
+constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16, kLhTs = 4 * kTile + 16;
 
 struct TileLds {
     size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, ctr, total;
@@ -392,17 +393,19 @@ __device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t 
                                             int& xlo, int& xhi) {
     const int cb = cur >> 3;
     const int32_t sl = LH[kLhSuf + cur], sh = LH[kLhSuf + kTile + cur];
+    const int32_t tl = LH[kLhTs + cur], th = LH[kLhTs + kTile + cur];
     const int4 n0 = ld4(LH + kLhBx), n1 = ld4(LH + kLhBx + 4);
     const int4 x0 = ld4(LH + kLhBx + 8), x1 = ld4(LH + kLhBx + 12);
-    asm volatile("" ::"v"(sl), "v"(sh));
+    asm volatile("" ::"v"(sl), "v"(sh), "v"(tl), "v"(th));
     pin4(n0); pin4(n1); pin4(x0); pin4(x1);
+    xlo = xhi = kTile;
+    // the tile-suffix extrema tell at once whether a level is touched in [cur, 63]: a wave
+    // whose lanes all miss (mostly its last iteration of the tile, carrying open trades past
+    // its end) skips the block tests and round 2
+    if (!__ballot(tl <= XL || th > XH1)) return;
     const uint32_t after = (0xFEu << cb) & 0xFFu;
     const bool inL = sl <= XL, inH = sh > XH1;
     const uint32_t laL = ~gt8(n0, n1, XL) & after, laH = gt8(x0, x1, XH1) & after;
-    xlo = xhi = kTile;
-    // round 2 only when some lane of the wave has a hit in the tile (not in a wave's last
-    // iteration, which mostly carries open trades past the tile end)
-    if (!__ballot(inL || inH || laL || laH)) return;
     // block to scan per side (cb when the hit is in cur's block; unused when there is none)
     const int fL = inL ? cb : (laL ? __builtin_ctz(laL) : cb);
     const int fH = inH ? cb : (laH ? __builtin_ctz(laH) : cb);
@@ -559,6 +562,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         }
         LH[kLhSuf + lane] = smn;
         LH[kLhSuf + kTile + lane] = smx;
+        // ... and to the end of the tile (one test tells whether a level is touched at all)
+        int32_t tmn = lv, tmx = hv;
+#pragma unroll
+        for (int d = 1; d < kTile; d <<= 1) {
+            const int32_t on = __shfl_down(tmn, d, 64), ox = __shfl_down(tmx, d, 64);
+            if (lane + d < kTile) {
+                tmn = min(tmn, on);
+                tmx = max(tmx, ox);
+            }
+        }
+        LH[kLhTs + lane] = tmn;
+        LH[kLhTs + kTile + lane] = tmx;
     };
 
     // with two or more task-only waves the parameter waves only walk (at raised priority)
@@ -749,7 +764,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const int32_t px = hit ? ((xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1) : cT[x];
                 // qi < a.sb only for a fill at the first bar of the tile of a carried position;
                 // a trade opened in this tile exits after its entry bar a.sb, so qi >= a.sb
-                const Agg seg = dst_query_bf(D, a.sb, FIRST ? max(qi, a.sb) : qi);
+                const Agg seg = dst_query_w(D, a.sb, FIRST ? max(qi, a.sb) : qi);
                 const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
                 const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
                 const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
