@@ -174,6 +174,8 @@ def main():
     ap.add_argument("--symbols", type=int, default=None,
                     help="override: symbols per GPU (weak) or in total (strong)")
     ap.add_argument("--leg", choices=["kernel", "ingest"], default="kernel")
+    ap.add_argument("--topk", type=int, default=TOPK,
+                    help="0 skips the top-k chain (profiling-build ablations, where Sharpes tie)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.leg == "ingest":
@@ -210,13 +212,14 @@ def main():
 
     grid = cfg["grid"]()
     P = grid.n_params
-    eng = D.Engine(grid, device=device, topk=TOPK, timing=True)
+    topk = args.topk
+    eng = D.Engine(grid, device=device, topk=topk, timing=True)
     eng.load_synthetic(SEED, sym0, n_sym, BARS, cfg["freq"])
     exchange = "none"
     if dist is not None:
         if dist.get_backend() == "nccl":
             try:  # the C-ABI exchange (RCCL from the engine's device buffers)
-                comm = PAR.make_comm(dist, device, TOPK)
+                comm = PAR.make_comm(dist, device, max(topk, 1))
                 exchange = "RCCL all-gather via bt_exchange (C ABI)"
             except Exception as why:  # noqa: BLE001 — fall back to torch's RCCL all-gather
                 print(f"bt_comm unavailable ({why}); exchanging over torch.distributed", file=sys.stderr)
@@ -225,12 +228,16 @@ def main():
 
     def issue(i):
         eng.run()                      # kernels of step i, enqueued on the engine stream
+        if topk == 0:
+            return
         if comm is not None:
             comm.exchange_async(eng, i & 1)   # RCCL all-gather behind the run's top-k chain
         else:
             eng.topk_fetch_async(i & 1)       # its top-k + trade count into pinned slot i % 2
 
     def finish(i):
+        if topk == 0:
+            return None
         if comm is not None:
             top, _ = comm.exchange_wait(i & 1)
             return top
