@@ -1,5 +1,6 @@
 #!/bin/bash
 # Interleaved A/B of an environment knob on the config-2 bench: VAR unset vs VAR=$VAL, R rounds.
+export BT_LIB=${BT_LIB:-libbt_prof.so}  # profiling build (make PROFILING=1)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 for r in $(seq ${R:-3}); do for m in unset set; do
   if [ $m = set ]; then export $VAR=$VAL; else unset $VAR; fi

@@ -2,6 +2,8 @@
 (config 4 on 8 GPUs: 250 symbols; config 3 on 2 GPUs: 250 symbols).   python scripts/lpw_probe.py"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
+os.environ.setdefault("BT_LIB", "libbt_prof.so")
 import dbx_amd as D
 for cfg, S in ((4, 250), (3, 250), (4, 500)):
     for lpw in (64, 32, 16):

@@ -2,6 +2,8 @@
 4-GPU (500 symbols) config-4 shards.   python scripts/xw_probe.py"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
+os.environ.setdefault("BT_LIB", "libbt_prof.so")
 import dbx_amd as D
 for S in (250, 500):
     for xw in (0, 2, 3, 4, 6):
