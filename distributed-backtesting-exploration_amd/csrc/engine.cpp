@@ -97,7 +97,9 @@ struct bt_engine {
     // Bollinger bar segments (k_tile.hip): requested count (0 = auto, 1 = off), burn-in tiles,
     // the records of a split run and the count the last run used
     int32_t seg_req = 0, seg_burn = kDefaultBurnTiles, seg_last = 1;
+    bool seg_burn_set = false;
     DevBuf<SegRec> d_seg;
+    DevBuf<double> d_segema;
     DevBuf<unsigned long long> d_refixed;
     DevBuf<unsigned long long> d_dbg;
     // top-k chain stream: the chain of run i overlaps the kernel of run i+1
@@ -351,11 +353,30 @@ void run_impl(bt_engine* e) {
         case BT_SMA_CROSS:
             err = launch_sma(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
             break;
-        case BT_EMA_OLS:
-            err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
+        case BT_EMA_OLS: {
+            int32_t maxspan = 1, maxb = 0;
+            for (int32_t v : e->ax[0]) maxspan = std::max(maxspan, v);
+            for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);
+            // the default burn-in lets every span's chain meet the true one; an explicit one
+            // (bt_set_segments) is honoured, the fix pass covering a short one
+            const int32_t burn = e->seg_burn_set ? e->seg_burn : ema_burn_tiles(maxspan);
+            SegArgs sg{nullptr, nullptr, nullptr, 1, burn};
+            if (!parity) sg.G = e->seg_req > 0 ? e->seg_req : ema_auto_segments(S, e->P, maxb, burn);
+            if (sg.G > 1) {
+                e->d_seg.ensure((size_t)sg.G * S * e->P);
+                e->d_segema.ensure((size_t)sg.G * S * kEmaSegStride);
+                e->d_refixed.ensure(1);
+                HIPCHK(hipMemsetAsync(e->d_refixed.p, 0, sizeof(unsigned long long), e->stream));
+                sg.rec = e->d_seg.p;
+                sg.refixed = e->d_refixed.p;
+                sg.ema = e->d_segema.p;
+            }
+            e->seg_last = sg.G;
+            err = launch_ema_ols(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, sg, e->stream);
             break;
+        }
         case BT_BOLL: {
-            SegArgs sg{nullptr, nullptr, 1, e->seg_burn};
+            SegArgs sg{nullptr, nullptr, nullptr, 1, e->seg_burn};
             if (!parity) {
                 int32_t maxb = 0;
                 for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);
@@ -795,6 +816,7 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_sums.release();
         e->d_trades.release();
         e->d_seg.release();
+        e->d_segema.release();
         e->d_refixed.release();
         e->d_dbg.release();
         e->d_hist.release();
@@ -833,6 +855,7 @@ int32_t bt_set_segments(bt_engine* e, int32_t segments, int32_t burn_tiles) {
         if (!e || segments < 0 || segments > 64 || burn_tiles < 0) throw HipFail{"bad arguments"};
         e->seg_req = segments;
         e->seg_burn = burn_tiles > 0 ? burn_tiles : kDefaultBurnTiles;
+        e->seg_burn_set = burn_tiles > 0;
         return 0;
     })
 }

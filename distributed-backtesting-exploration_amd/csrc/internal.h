@@ -57,23 +57,7 @@ struct Out {
     unsigned long long* dbg;       // profiling stamps (Grid::ablate & 64), else nullptr
 };
 
-// Launchers (k_*.hip). All enqueue on `st` and return hipError_t.
-hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
-                      int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st);
-size_t sma_lds_bytes(const Grid& g);  // dynamic LDS of the SMA kernel for this grid
-struct SmaShape {                     // SMA launch shape for P parameters (k_sma.hip)
-    int pw;                           // parameter waves per block
-    int dedicated;                    // 1: an extra helper wave runs the tile scan
-    int block, gy;                    // threads per block, y-blocks per symbol
-};
-SmaShape sma_shape(int P);
-hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                      const Out& out, bool parity, hipStream_t st);
-size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
-size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
-hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                          const Out& out, bool parity, hipStream_t st);
-// Bar-axis split of the Bollinger walk (k_tile.hip): each symbol's tiles are cut into G
+// Bar-axis split of the tile kernels (k_tile.hip): each symbol's tiles are cut into G
 // segments walked by separate workgroups. Segment s >= 1 starts flat `burn_tiles` tiles before
 // its first bar (a walk whose accounting is discarded) and records the state it reached there;
 // a fix pass per boundary re-walks a segment from the true state (the previous segment's end)
@@ -98,10 +82,33 @@ static_assert(sizeof(SegRec) == 128, "SegRec layout");
 struct SegArgs {
     SegRec* rec;
     unsigned long long* refixed;   // fix-pass blocks that re-walked their segment
+    double* ema;                   // EMA+OLS: per (segment, symbol) the chains' values entering
+                                   // the segment [0, 64) and leaving it [64, 128), lane = span
     int32_t G;                     // segments per symbol (1 = no split)
     int32_t burn_tiles;            // tiles walked before a speculative segment's first bar
 };
 constexpr int kDefaultBurnTiles = 64;
+constexpr int kEmaSegStride = 128;  // doubles per (segment, symbol) in SegArgs::ema
+// Launchers (k_*.hip). All enqueue on `st` and return hipError_t.
+hipError_t launch_gen(const SymDesc* syms, int32_t n_sym, uint64_t seed, int32_t freq,
+                      int32_t* o, int32_t* h, int32_t* l, int32_t* c, hipStream_t st);
+size_t sma_lds_bytes(const Grid& g);  // dynamic LDS of the SMA kernel for this grid
+struct SmaShape {                     // SMA launch shape for P parameters (k_sma.hip)
+    int pw;                           // parameter waves per block
+    int dedicated;                    // 1: an extra helper wave runs the tile scan
+    int block, gy;                    // threads per block, y-blocks per symbol
+};
+SmaShape sma_shape(int P);
+hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                      const Out& out, bool parity, hipStream_t st);
+size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
+size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
+hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                          const Out& out, bool parity, const SegArgs& seg, hipStream_t st);
+// EMA+OLS segments: count for this shard (auto mode) and the burn-in a speculative segment needs
+// for every span's fp64 chain to meet the true one bit for bit (~16 spans of bars measured).
+int32_t ema_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int32_t burn_tiles);
+int32_t ema_burn_tiles(int32_t max_span);
 hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, const int32_t* low,
                        const int32_t* close, const Grid& g, const Out& out, bool parity,
                        const SegArgs& seg, hipStream_t st);

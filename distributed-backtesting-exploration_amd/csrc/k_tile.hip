@@ -111,10 +111,16 @@ __device__ __forceinline__ uint64_t bits_from(int cur) { return cur < kTile ? (~
 //           counter;
 //   parameter waves, tile k: one trade per loop iteration (entry at the first entry bar, exit
 //           at the first exit bar), O(1) accounting per trade.
-template <bool PARITY, bool STAMPS>
+// SEG: bar segments as in boll_tile_kernel; besides the lanes' trade states a segment's start
+// must agree on the EMA chains: a speculative segment starts each chain at its first scanned bar
+// (e = c there) and records the values entering its first accounted bar; fp64 chains from
+// different starts meet bit for bit after ~16 spans of bars (the burn-in covers 24), after which
+// they are identical. The fix pass compares them too and re-walks from the true values.
+template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
-                                                        Grid g, Out out, int nextra, int lpw) {
+                                                        Grid g, Out out, int nextra, int lpw,
+                                                        SegArgs sg, int fix_seg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nsp = g.na, nol = g.nb, R = g.ring;
     const TileLds LL = tile_lds_layout(0, R, nsp, nol);
@@ -144,18 +150,53 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int nword = 4 * nsp + 2 * nol, ntask = max(nsp, nol);
     const int estage = nsp * kEStride;
 
+    SegRange sr{0, 0, 0, 0, ntiles};
+    const SegRec* prev = nullptr;
+    SegRec* mine = nullptr;
+    double* ema_mine = nullptr;        // this (segment, symbol)'s chain record
+    const double* ema_prev = nullptr;  // the previous segment's
+    if (SEG) {
+        sr = seg_range(sg, fix_seg, ntiles, g.wmax);
+        const size_t per_seg = (size_t)gridDim.x * P;
+        mine = sg.rec + sr.seg * per_seg + (size_t)blockIdx.x * P + pj;
+        ema_mine = sg.ema + ((size_t)sr.seg * gridDim.x + blockIdx.x) * kEmaSegStride;
+        if (sr.seg > 0) {
+            prev = mine - per_seg;
+            ema_prev = ema_mine - (size_t)gridDim.x * kEmaSegStride;
+        }
+        if (fix_seg > 0) {  // re-walk if a lane's state or a span's chain value is not the true one
+            const bool lane_differs = active && seg_start_differs(mine, prev);
+            const bool chain_differs = helperB && lane < nsp && ema_mine[lane] != ema_prev[64 + lane];
+            if (!__syncthreads_or(lane_differs || chain_differs)) return;
+            if (tid == 0) atomicAdd(sg.refixed, 1ULL);
+        }
+    }
+    const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
+    // the chains start at bar chain_b0 with e = c there (bar 0, or a speculative segment's first
+    // scanned bar); the fix pass instead starts them at its first bar from the true values
+    const bool chain_injected = SEG && fix_seg > 0;
+    const int chain_b0 = chain_injected ? -1 : T_scan * kTile;
+    const int chain_T0 = chain_injected ? T_acct : T_scan;
+
     for (int o = tid; o < nol; o += blockDim.x) win[o] = g.b[o];
     if (tid == 0) {
-        r1[0] = r2[0] = 0;
-        *ctr = 0;
+        // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
+        r1[(T_scan * kTile) % R] = 0;
+        r2[(T_scan * kTile) % R] = 0;
+        // task rounds are numbered by tile (flags): the counter starts at round T_scan
+        const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
+        *ctr = (uint32_t)T_scan * (uint32_t)(ntask + ngrab0);
     }
-    double alpha = 0.0, ema = 0.0;
-    if (helperB && lane < nsp) alpha = 2.0 / ((double)g.a[lane] + 1.0);
+    double alpha = 0.0, ema = 0.0, ema_start = 0.0;
+    if (helperB && lane < nsp) {
+        alpha = 2.0 / ((double)g.a[lane] + 1.0);
+        if (chain_injected) ema = ema_start = ema_prev[64 + lane];
+    }
     const int winreg = lane < nol ? g.b[lane] : 1;  // OLS window lengths, lane = window
     const double lo_mult = (double)(10000 - g.band_bps), hi_mult = (double)(10000 + g.band_bps);
     __syncthreads();
 
-    TileCarry cy{0, 0};
+    TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     uint64_t cy2 = 0;
     int32_t cpre = 0;
 
@@ -174,13 +215,14 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     // loads itself (no dependency on helper A's scan of the same tile):
     // e_t = e_{t-1} + alpha (c_t - e_{t-1}), three roundings, e_0 = c_0
     auto chain = [&](int T, int32_t cl) {
+        if (SEG && T < chain_T0) return;  // fix pass: bars before the segment are not needed
         const int t1 = T * kTile;
         double* E = ebuf + (T & 1) * estage + lane * kEStride;
         // the chain is the block's per-tile critical path (three dependent fp64 operations per
         // bar): issue it ahead of the other waves on its SIMD
         if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(3);
         if (lane < nsp) {
-            if (t1 > 0 && t1 + kTile <= B) {
+            if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
 #pragma unroll
                 for (int b = 0; b < kTile; ++b) {
                     const double cd = (double)__builtin_amdgcn_readlane(cl, b);
@@ -191,10 +233,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 #pragma unroll 1
                 for (int b = 0; b < kTile; ++b) {
                     const double cd = (double)__builtin_amdgcn_readlane(cl, b);
-                    if (t1 + b < B) ema = (t1 + b == 0) ? cd : ema + alpha * (cd - ema);
+                    if (t1 + b < B) ema = (t1 + b == chain_b0) ? cd : ema + alpha * (cd - ema);
                     E[b] = ema;
                 }
             }
+            if (SEG && T + 1 == T_acct) ema_start = ema;  // the values entering the first accounted bar
         }
         __builtin_amdgcn_s_setprio(0);
     };
@@ -254,35 +297,49 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         }
     };
 
-    // prologue: scan + chain tiles 0, 1; words of tile 0
+    // prologue: scan + chain the first two tiles; words of the first
     if (helperA || helperB) {
-        const int32_t c0 = ldc(crow, B, lane, 0), c1 = ldc(crow, B, kTile + lane, 0);
-        cpre = ldc(crow, B, 2 * kTile + lane, 0);
-        if (helperA) scan(0, c0); else chain(0, c0);
-        if (ntiles > 1) {
-            if (helperA) scan(1, c1); else chain(1, c1);
+        const int b0 = T_scan * kTile;
+        const int32_t c0 = ldc(crow, B, b0 + lane, 0), c1 = ldc(crow, B, b0 + kTile + lane, 0);
+        cpre = ldc(crow, B, b0 + 2 * kTile + lane, 0);
+        if (T_scan < T_end) {
+            if (helperA) scan(T_scan, c0); else chain(T_scan, c0);
+        }
+        if (T_scan + 1 < T_end) {
+            if (helperA) scan(T_scan + 1, c1); else chain(T_scan + 1, c1);
         }
     }
     __syncthreads();
-    flags(0);
+    if (T_scan < T_end) flags(T_scan);
     __syncthreads();
 
     TradeAcct a;
     acct_init(a);
+    int32_t start_pos = 0, start_e = 0;  // SEG: state at the first accounted bar
+    if (SEG && fix_seg > 0 && active) {
+        seg_inject(a, prev);
+        start_pos = a.pos;
+        start_e = a.e;
+    }
     const size_t gi = (size_t)blockIdx.x * P + pj;
     bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
 
     StampAcc sa;
     if (STAMPS) sa.begin();
-    for (int k = 0; k < ntiles; ++k) {
+    for (int k = T_scan; k < T_end; ++k) {
         const int t0 = k * kTile;
-        if ((helperA || helperB) && k + 2 < ntiles) {
+        if ((helperA || helperB) && k + 2 < T_end) {
             if (helperA) scan(k + 2, cpre); else chain(k + 2, cpre);
             cpre = ldc(crow, B, t0 + 3 * kTile + lane, 0);
         }
         if (STAMPS) sa.mark(0);
-        if (active && !BT_ABL(g, 8)) {
+        if (SEG && k == T_acct && active) {
+            start_pos = a.pos;
+            start_e = a.e;
+            seg_reset_sums(a);
+        }
+        if (active && k >= T_walk && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
@@ -323,7 +380,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 const Agg seg = dst_query_bf(D, a.sb, x);
                 const Agg st = FIRST ? agg_merge(a.agg, seg) : seg;
                 const bool lg = a.pos > 0;
-                acct_close<PARITY>(a, t0 + x, cx, st, tr, cap);
+                acct_close<PARITY, SEG>(a, t0 + x, cx, st, tr, cap);
                 a.ps1 += lg ? qx : (uint64_t)0 - qx;
                 a.ps2 += q2x;
                 a.pos = 0;
@@ -339,12 +396,20 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !BT_ABL(g, 2)) flags(k + 1);
+        if (k + 1 < T_end && !BT_ABL(g, 2)) flags(k + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
     }
     if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helperA ? 1 : (helperB ? 2 : 3)), lane);
+    if (SEG) {
+        if (active) seg_write(a, start_pos, start_e, mine);
+        if (helperB && lane < nsp) {
+            ema_mine[lane] = ema_start;
+            ema_mine[64 + lane] = ema;  // after the segment's last bar
+        }
+        return;
+    }
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
     wave_add_trades(out, active ? a.ntr : 0);
 }
@@ -429,7 +494,7 @@ __device__ __forceinline__ double level_y(double ce, double g) { return ce * g +
 // SEG: one bar segment per block (blockIdx.z = segment; or, with fix_seg >= 1, the fix pass of
 // boundary fix_seg: the block re-walks that segment from the previous segment's end states if
 // any lane's speculative start differs, and otherwise returns at once). Results go to SegRec
-// records (internal.h) that boll_seg_combine folds.
+// records (internal.h) that seg_combine folds.
 template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
                                                          const int32_t* __restrict__ high,
@@ -482,30 +547,20 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     // tiles of this block: scanned from T_scan (every window of the first walked bar complete),
     // walked from T_walk, accounted from T_acct, up to T_end (exclusive)
-    int T_scan = 0, T_walk = 0, T_acct = 0, T_end = ntiles, seg = 0;
+    SegRange sr{0, 0, 0, 0, ntiles};
     const SegRec* prev = nullptr;
     SegRec* mine = nullptr;
     if (SEG) {
-        seg = fix_seg > 0 ? fix_seg : (int)blockIdx.z;
-        T_acct = (int)((int64_t)seg * ntiles / sg.G);
-        T_end = (int)((int64_t)(seg + 1) * ntiles / sg.G);
-        T_walk = (fix_seg > 0 || seg == 0) ? T_acct : max(0, T_acct - sg.burn_tiles);
-        T_scan = max(0, T_walk - (g.wmax - 1 + kTile - 1) / kTile);
-        if (T_acct >= T_end) T_scan = T_walk = T_acct = T_end;  // empty segment: state passes through
+        sr = seg_range(sg, fix_seg, ntiles, g.wmax);
         const size_t per_seg = (size_t)gridDim.x * P;
-        mine = sg.rec + seg * per_seg + (size_t)blockIdx.x * P + pj;
-        if (seg > 0) prev = mine - per_seg;
-        if (fix_seg > 0) {
-            // the fix pass re-walks only if some lane's speculative start state is not the true one
-            bool differs = false;
-            if (active) {
-                const int tp = prev->end_pos, te = prev->end_e;
-                differs = !(mine->start_pos == tp && (tp == 0 || mine->start_e == te));
-            }
-            if (!__syncthreads_or(differs)) return;
+        mine = sg.rec + sr.seg * per_seg + (size_t)blockIdx.x * P + pj;
+        if (sr.seg > 0) prev = mine - per_seg;
+        if (fix_seg > 0) {  // re-walk only if some lane's speculative start is not the true one
+            if (!__syncthreads_or(active && seg_start_differs(mine, prev))) return;
             if (tid == 0) atomicAdd(sg.refixed, 1ULL);
         }
     }
+    const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
 
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
     for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
@@ -672,11 +727,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     };
     int32_t start_pos = 0, start_e = 0;  // SEG: state at the first accounted bar
     if (SEG && fix_seg > 0 && active) {  // the true state entering the segment
-        a.pos = prev->end_pos;
-        a.e = prev->end_e;
-        a.ce = prev->end_ce;
-        a.agg = Agg{prev->end_agg[0], prev->end_agg[1], prev->end_agg[2], prev->end_agg[3]};
-        a.sb = 0;
+        seg_inject(a, prev);
         if (a.pos != 0) set_levels(a.ce, a.pos);
         start_pos = a.pos;
         start_e = a.e;
@@ -702,13 +753,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             // burn-in's sums (a trade open here is closed and accounted in this segment)
             start_pos = a.pos;
             start_e = a.e;
-            a.R = 0;
-            a.A = 0;
-            a.Bq = a.C = a.D = kNegInf;
-            a.ntr = a.expo = 0;
-            a.h = 0;
-            a.s1 = a.s2 = 0;
-            a.ps1 = a.ps2 = 0;
+            seg_reset_sums(a);
         }
         if (active && k >= T_walk && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
@@ -791,32 +836,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     }
     if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helper ? 1 : 3), lane);
     if (SEG) {
-        if (active) {
-            SegRec r;
-            r.ntr = a.ntr;
-            r.expo = a.expo;
-            r.start_pos = start_pos;
-            r.start_e = start_e;
-            r.end_pos = a.pos;
-            r.end_e = a.e;
-            r.end_ce = a.ce;
-            r.pad = 0;
-            r.end_agg[0] = a.agg.mx;
-            r.end_agg[1] = a.agg.mn;
-            r.end_agg[2] = a.agg.dd;
-            r.end_agg[3] = a.agg.du;
-            r.R = a.R;
-            r.A = a.A;
-            r.B = a.Bq;
-            r.C = a.C;
-            r.D = a.D;
-            r.h = a.h;
-            r.s1lo = (uint64_t)a.s1;
-            r.s1hi = (int64_t)(a.s1 >> 64);
-            r.s2lo = (uint64_t)a.s2;
-            r.s2hi = (int64_t)(a.s2 >> 64);
-            *mine = r;
-        }
+        if (active) seg_write(a, start_pos, start_e, mine);
         return;
     }
     if (active) acct_write(a, B, g.sqrt_ann, gi, out);
@@ -825,7 +845,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
 // Folds the bar segments of every (symbol, param) in order: additive counts, pnl, hash and
 // return sums; the drawdown forms composed from g = m = 0 (tile_common.h TradeAcct).
-__global__ __launch_bounds__(256) void boll_seg_combine(const SymDesc* __restrict__ syms,
+__global__ __launch_bounds__(256) void seg_combine(const SymDesc* __restrict__ syms,
                                                         int n_sym, int P, const SegRec* __restrict__ rec,
                                                         int G, double sqrt_ann, Out out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -911,25 +931,51 @@ static int tile_extra_waves(int used, int x) {
 size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
 size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g.nb).total; }
 
+int32_t ema_burn_tiles(int32_t max_span) {
+    // two fp64 EMA chains from different starts met bit for bit after 131-162 bars (span 10)
+    // to 11,559-13,368 bars (span 780) over 18 starts each (round-2 measurement): 24 spans
+    return std::max(kDefaultBurnTiles, (24 * max_span + kTile - 1) / kTile);
+}
+
+int32_t ema_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int32_t burn_tiles) {
+    if (n_sym <= 0) return 1;
+    const int pw = std::min((n_params + 63) / 64, 1024 / 64 - 2);
+    const long long blocks = (long long)n_sym * ((n_params + 64 * pw - 1) / (64 * pw));
+    if (blocks > device_cus()) return 1;
+    int G = (int)std::min<long long>(4, std::max<long long>(1, 2LL * device_cus() / blocks));
+    const int ntiles = (max_bars + kTile - 1) / kTile;
+    while (G > 1 && ntiles / G < 2 * burn_tiles) --G;
+    return G;
+}
+
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                          const Out& out, bool parity, hipStream_t st) {
+                          const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
     const int lpw = tile_lanes_per_wave();
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 2);
     const int xw = tile_extra_waves(pw + 2, 5);
-    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw));
+    const bool split = seg.G > 1 && !parity;
+    const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw), split ? seg.G : 1);
     const dim3 block(64 * (pw + 2 + xw));
     const size_t lds = ema_lds_bytes(g);
 #ifdef BT_PROFILING
     if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((ema_tile_kernel<false, true>), grid, block, lds, st, syms, close, g, out, xw, lpw);
+        hipLaunchKernelGGL((ema_tile_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
         return hipGetLastError();
     }
 #endif
-    if (parity)
-        hipLaunchKernelGGL((ema_tile_kernel<true, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
-    else
-        hipLaunchKernelGGL((ema_tile_kernel<false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw);
+    if (split) {
+        hipLaunchKernelGGL((ema_tile_kernel<false, false, true>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+        const dim3 fgrid(grid.x, grid.y, 1);
+        for (int s = 1; s < seg.G; ++s)
+            hipLaunchKernelGGL((ema_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, close, g, out, xw, lpw, seg, s);
+        const size_t n = (size_t)n_sym * g.n_params;
+        hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
+    } else if (parity) {
+        hipLaunchKernelGGL((ema_tile_kernel<true, false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+    } else {
+        hipLaunchKernelGGL((ema_tile_kernel<false, false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+    }
     return hipGetLastError();
 }
 
@@ -977,7 +1023,7 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
         for (int s = 1; s < seg.G; ++s)
             hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s);
         const size_t n = (size_t)n_sym * g.n_params;
-        hipLaunchKernelGGL(boll_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
+        hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
     } else if (parity) {
         hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
     } else {

@@ -164,6 +164,80 @@ __device__ __forceinline__ void acct_write(const TradeAcct& a, int bars, double 
     if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
 }
 
+// ---- bar segments (SegRec / SegArgs in internal.h; used by both tile kernels)
+// Tiles of one block: scanned from T_scan (every window of the first walked bar complete),
+// walked from T_walk, accounted from T_acct, up to T_end (exclusive). Speculative segments
+// s >= 1 walk `burn` tiles before their first bar; the fix pass (fix_seg = s) walks segment s
+// from its first bar.
+struct SegRange {
+    int seg, T_scan, T_walk, T_acct, T_end;
+};
+
+__device__ __forceinline__ SegRange seg_range(const SegArgs& sg, int fix_seg, int ntiles, int wmax) {
+    SegRange r;
+    r.seg = fix_seg > 0 ? fix_seg : (int)blockIdx.z;
+    r.T_acct = (int)((int64_t)r.seg * ntiles / sg.G);
+    r.T_end = (int)((int64_t)(r.seg + 1) * ntiles / sg.G);
+    r.T_walk = (fix_seg > 0 || r.seg == 0) ? r.T_acct : max(0, r.T_acct - sg.burn_tiles);
+    r.T_scan = max(0, r.T_walk - (wmax - 1 + kTile - 1) / kTile);
+    if (r.T_acct >= r.T_end) r.T_scan = r.T_walk = r.T_acct = r.T_end;  // no bars: state passes through
+    return r;
+}
+
+// Do a lane's speculative start and the true state entering its segment differ? Two walks in
+// the same state at a bar (flat, or in the trade entered at the same bar) agree from then on.
+__device__ __forceinline__ bool seg_start_differs(const SegRec* mine, const SegRec* prev) {
+    const int tp = prev->end_pos, te = prev->end_e;
+    return !(mine->start_pos == tp && (tp == 0 || mine->start_e == te));
+}
+
+// The true state entering the segment (fix pass).
+__device__ __forceinline__ void seg_inject(TradeAcct& a, const SegRec* prev) {
+    a.pos = prev->end_pos;
+    a.e = prev->end_e;
+    a.ce = prev->end_ce;
+    a.agg = Agg{prev->end_agg[0], prev->end_agg[1], prev->end_agg[2], prev->end_agg[3]};
+    a.sb = 0;
+}
+
+// First accounted tile: the sums restart (the burn-in's are dropped); the state carries on.
+__device__ __forceinline__ void seg_reset_sums(TradeAcct& a) {
+    a.R = 0;
+    a.A = 0;
+    a.Bq = a.C = a.D = kNegInf;
+    a.ntr = a.expo = 0;
+    a.h = 0;
+    a.s1 = a.s2 = 0;
+    a.ps1 = a.ps2 = 0;
+}
+
+__device__ __forceinline__ void seg_write(const TradeAcct& a, int start_pos, int start_e, SegRec* mine) {
+    SegRec r;
+    r.ntr = a.ntr;
+    r.expo = a.expo;
+    r.start_pos = start_pos;
+    r.start_e = start_e;
+    r.end_pos = a.pos;
+    r.end_e = a.e;
+    r.end_ce = a.ce;
+    r.pad = 0;
+    r.end_agg[0] = a.agg.mx;
+    r.end_agg[1] = a.agg.mn;
+    r.end_agg[2] = a.agg.dd;
+    r.end_agg[3] = a.agg.du;
+    r.R = a.R;
+    r.A = a.A;
+    r.B = a.Bq;
+    r.C = a.C;
+    r.D = a.D;
+    r.h = a.h;
+    r.s1lo = (uint64_t)a.s1;
+    r.s1hi = (int64_t)(a.s1 >> 64);
+    r.s2lo = (uint64_t)a.s2;
+    r.s2hi = (int64_t)(a.s2 >> 64);
+    *mine = r;
+}
+
 // Diagnostic s_memtime stamps (Grid::ablate & 64 builds only): per role (0 = parameter waves,
 // 1 = helper A, 2 = helper B) the cycles spent working and waiting at the tile barrier.
 // dbg[8 * role + {0, 1, 2..5, 7}] = work, barrier, marked segments / counts, waves.

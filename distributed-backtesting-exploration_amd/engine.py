@@ -301,7 +301,8 @@ class Engine:
         _check(lib().bt_run(self._h))
 
     def set_segments(self, segments: int, burn_tiles: int = 0) -> None:
-        """Bollinger bar-axis split: 0 = automatic, 1 = off, n = n segments per symbol."""
+        """Bar-axis split of the EMA+OLS / Bollinger walks: 0 = automatic, 1 = off, n = n
+        segments per symbol; burn_tiles 0 = the strategy's default burn-in."""
         _check(lib().bt_set_segments(self._h, segments, burn_tiles))
 
     def last_segments(self, with_refixed: bool = False):

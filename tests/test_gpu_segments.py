@@ -90,3 +90,63 @@ def test_parity_mode_never_splits():
         e.load_synthetic(0x5EED, 0, 2, 5000, D.BT_MINUTE)
         e.run()
         assert e.last_segments() == 1
+
+
+def _run_grid(grid, cols, segments, burn=0):
+    with D.Engine(grid) as e:
+        e.set_segments(segments, burn)
+        e.load_ohlc([x[3] for x in cols], [x[1] for x in cols], [x[2] for x in cols])
+        e.run()
+        got = e.summaries().copy()
+        used, refixed = e.last_segments(with_refixed=True)
+    return got, used, refixed
+
+
+@pytest.mark.parametrize("segments,burn", [(2, 0), (3, 0), (2, 1), (4, 2)])
+def test_ema_split_equals_unsplit_and_oracle(segments, burn):
+    """EMA+OLS segments must also agree on the fp64 EMA chains at every boundary: with the
+    default burn-in (24 x the longest span) the speculative chains meet the true ones; with a
+    1-2 tile burn-in they cannot, and the fix pass re-walks from the true chain values."""
+    grid = D.Grid.ema_ols([10, 60, 390], [15, 120, 780], band_bps=20)
+    cols = [F.gen(0x5EED, 60 + i, 40000, 1) for i in range(3)]
+    ref, used1, _ = _run_grid(grid, cols, 1)
+    got, used, refixed = _run_grid(grid, cols, segments, burn)
+    assert used1 == 1 and used == segments
+    if burn and burn <= 2:
+        assert refixed > 0
+    assert got.tobytes() == ref.tobytes(), "split run differs from the unsplit run"
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("ema_ols", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(grid.n_params):
+            compare_summary(got[i, p], orc[p], f"ema G={segments} burn={burn} sym {i} {grid.param(p)}")
+
+
+def test_ema_split_ragged_and_empty_segments():
+    grid = D.Grid.ema_ols([2, 3, 10, 100], [2, 4, 70, 200], band_bps=20)
+    lengths = [1, 2, 63, 64, 65, 130, 700, 5000]
+    cols = [F.gen(0x5EED, 80 + i, n, 1) for i, n in enumerate(lengths)]
+    ref, _, _ = _run_grid(grid, cols, 1)
+    for segments, burn in ((4, 1), (9, 1), (3, 0)):
+        got, used, _ = _run_grid(grid, cols, segments, burn)
+        assert used == segments and got.tobytes() == ref.tobytes(), (segments, burn)
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("ema_ols", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(grid.n_params):
+            compare_summary(ref[i, p], orc[p], f"ema ragged {lengths[i]} bars {grid.param(p)}")
+
+
+def test_ema_auto_split_config3_grid_small_shard():
+    """Config-3 grid on a small shard (automatic split) against the oracle on sampled symbols."""
+    grid = D.config3_grid()
+    with D.Engine(grid) as e:
+        e.load_synthetic(0x5EED, 200, 100, 98280, D.BT_MINUTE)
+        e.run()
+        got = e.summaries().copy()
+        used, refixed = e.last_segments(with_refixed=True)
+    assert used >= 2
+    print(f"config-3 grid, 100 symbols: {used} segments, {refixed} boundary blocks re-walked")
+    for s in (0, 63, 99):
+        o, h, lo, c = F.gen(0x5EED, 200 + s, 98280, 1)[:4]
+        orc, _ = oracle_row("ema_ols", grid, (o, h, lo, c), 98280)
+        for p in range(0, grid.n_params, 3):
+            compare_summary(got[s, p], orc[p], f"ema auto split sym {200 + s} {grid.param(p)}")
