@@ -173,11 +173,20 @@ struct SegRange {
     int seg, T_scan, T_walk, T_acct, T_end;
 };
 
+// Boundaries balance the walked tiles: segment 0 (no burn-in) is `burn` tiles longer than the
+// others, so every segment walks about (ntiles + (G - 1) burn) / G tiles.
+__device__ __forceinline__ int seg_start(int s, int G, int ntiles, int burn) {
+    if (s <= 0) return 0;
+    if (s >= G) return ntiles;
+    const int x = (ntiles - burn) / G;
+    return x > 0 ? burn + s * x : (int)((int64_t)s * ntiles / G);
+}
+
 __device__ __forceinline__ SegRange seg_range(const SegArgs& sg, int fix_seg, int ntiles, int wmax) {
     SegRange r;
     r.seg = fix_seg > 0 ? fix_seg : (int)blockIdx.z;
-    r.T_acct = (int)((int64_t)r.seg * ntiles / sg.G);
-    r.T_end = (int)((int64_t)(r.seg + 1) * ntiles / sg.G);
+    r.T_acct = seg_start(r.seg, sg.G, ntiles, sg.burn_tiles);
+    r.T_end = seg_start(r.seg + 1, sg.G, ntiles, sg.burn_tiles);
     r.T_walk = (fix_seg > 0 || r.seg == 0) ? r.T_acct : max(0, r.T_acct - sg.burn_tiles);
     r.T_scan = max(0, r.T_walk - (wmax - 1 + kTile - 1) / kTile);
     if (r.T_acct >= r.T_end) r.T_scan = r.T_walk = r.T_acct = r.T_end;  // no bars: state passes through
