@@ -101,10 +101,8 @@ def host_cpus():
 def cpu_baseline(cfg, grid, sym0, shard, target_thread_s=25.0, target_1t_s=8.0):
     """The C oracle (oracle/oracle.c, -O2 -ffp-contract=off) on the first symbols of
     rank 0's shard of the same workload, on 1 thread and on every usable host CPU, each sample
-    sized from a one-symbol probe (~8 s on one thread, ~25 thread-seconds on all). SMA grids run
-    on the oracle's pthread grid (one symbol per task); EMA/Bollinger run one (symbol, param)
-    call per task on a thread pool (ctypes releases the GIL)."""
-    from concurrent.futures import ThreadPoolExecutor
+    sized from a one-symbol probe (~8 s on one thread, ~25 thread-seconds on all), on the
+    oracle's pthread pool (orc_*_grid_mt: one task per symbol, every param of it)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc_ffi as F
     cpus = host_cpus()
@@ -119,20 +117,15 @@ def cpu_baseline(cfg, grid, sym0, shard, target_thread_s=25.0, target_1t_s=8.0):
     def run(n, threads):
         cs = cols(n)
         t0 = time.perf_counter()
+        closes = np.stack([x[3] for x in cs])
         if grid.strategy == D.BT_SMA_CROSS:
-            F.sma_grid_mt(np.stack([x[3] for x in cs]), np.asarray(grid.axes[0]),
-                          np.asarray(grid.axes[1]), ann, threads)
+            F.sma_grid_mt(closes, grid.axes[0], grid.axes[1], ann, threads)
+        elif grid.strategy == D.BT_EMA_OLS:
+            F.ema_grid_mt(closes, grid.axes[0], grid.axes[1], grid.band_bps, ann, threads)
         else:
-            def one(sp):
-                s, p = sp
-                o, h, lo, c = cs[s][:4]
-                kw = grid.param(p)
-                if grid.strategy == D.BT_EMA_OLS:
-                    F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], ann)
-                else:
-                    F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], ann)
-            with ThreadPoolExecutor(threads) as ex:
-                list(ex.map(one, [(s, p) for s in range(n) for p in range(grid.n_params)]))
+            F.boll_grid_mt(np.stack([x[1] for x in cs]), np.stack([x[2] for x in cs]), closes,
+                           grid.axes[0], grid.axes[1], grid.k_den, grid.axes[2], grid.axes[3],
+                           ann, threads)
         return time.perf_counter() - t0
 
     per_sym = run(1, 1)  # one symbol on one thread: the probe
@@ -146,7 +139,7 @@ def cpu_baseline(cfg, grid, sym0, shard, target_thread_s=25.0, target_1t_s=8.0):
     return {"value": vA, "unit": "bar-evals/s", "cores": T, "kind": "port",
             "sample": f"first {nA} symbols of the shard x {B} bars x {grid.n_params} params on "
                       f"{T} threads ({dtA:.2f} s wall); 1 thread: first {n1} symbols ({dt1:.2f} s); "
-                      f"oracle/oracle.c, gcc -O2 -ffp-contract=off",
+                      f"oracle/oracle.c orc_*_grid_mt, gcc -O2 -ffp-contract=off",
             "value_1t": v1, "value_all": vA, "threads_all": T, "nproc": cpus["nproc"],
             "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["cgroup_quota_cpus"],
             "model": cpus["model"]}

@@ -494,3 +494,71 @@ void orc_sma_grid_mt(const int32_t* c, int32_t S, int32_t B, const int32_t* fast
     for (int32_t i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, mt_worker, &j);
     for (int32_t i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
 }
+
+/* EMA+OLS and Bollinger grids on the same pool: one task per symbol, every param of it in the
+ * engine's param order (include/bt.h). h and l may be NULL for EMA+OLS. */
+typedef struct mt_grid {
+    int32_t strategy; /* 2 = EMA+OLS, 3 = Bollinger */
+    const int32_t *h, *l, *c;
+    int32_t S, B;
+    const int32_t* ax[4];
+    int32_t n[4];
+    int32_t band_bps, k_den;
+    int64_t ann;
+    orc_summary* out;
+    int32_t next;
+    pthread_mutex_t mu;
+} mt_grid;
+
+static void* mt_grid_worker(void* arg) {
+    mt_grid* j = (mt_grid*)arg;
+    const int32_t P = j->n[0] * j->n[1] * j->n[2] * j->n[3];
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        const int32_t s = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (s >= j->S) break;
+        const size_t row = (size_t)s * j->B;
+        orc_summary* o = j->out + (size_t)s * P;
+        int32_t p = 0;
+        for (int32_t a = 0; a < j->n[0]; ++a)
+            for (int32_t b = 0; b < j->n[1]; ++b)
+                for (int32_t c = 0; c < j->n[2]; ++c)
+                    for (int32_t d = 0; d < j->n[3]; ++d, ++p) {
+                        if (j->strategy == 2)
+                            orc_ema_ols(j->c + row, j->B, j->ax[0][a], j->ax[1][b], j->band_bps,
+                                        j->ann, &o[p], NULL, 0);
+                        else
+                            orc_boll(j->h + row, j->l + row, j->c + row, j->B, j->ax[0][a],
+                                     j->ax[1][b], j->k_den, j->ax[2][c], j->ax[3][d], j->ann,
+                                     &o[p], NULL, 0);
+                    }
+    }
+    return NULL;
+}
+
+static void run_grid(mt_grid* j, int32_t nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int32_t i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, mt_grid_worker, j);
+    for (int32_t i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+}
+
+void orc_ema_grid_mt(const int32_t* c, int32_t S, int32_t B, const int32_t* span, int32_t nsp,
+                     const int32_t* ols, int32_t nol, int32_t band_bps, int64_t ann,
+                     orc_summary* out, int32_t nthreads) {
+    static const int32_t one = 0;
+    mt_grid j = {2, NULL, NULL, c, S, B, {span, ols, &one, &one}, {nsp, nol, 1, 1}, band_bps, 1,
+                 ann, out, 0, PTHREAD_MUTEX_INITIALIZER};
+    run_grid(&j, nthreads);
+}
+
+void orc_boll_grid_mt(const int32_t* h, const int32_t* l, const int32_t* c, int32_t S, int32_t B,
+                      const int32_t* win, int32_t nw, const int32_t* k_num, int32_t nk,
+                      int32_t k_den, const int32_t* sl, int32_t nsl, const int32_t* tp,
+                      int32_t ntp, int64_t ann, orc_summary* out, int32_t nthreads) {
+    mt_grid j = {3, h, l, c, S, B, {win, k_num, sl, tp}, {nw, nk, nsl, ntp}, 0, k_den,
+                 ann, out, 0, PTHREAD_MUTEX_INITIALIZER};
+    run_grid(&j, nthreads);
+}

@@ -71,6 +71,15 @@ void orc_boll(const int32_t* h, const int32_t* l, const int32_t* c, int32_t B,
 void orc_sma_grid_mt(const int32_t* c, int32_t S, int32_t B,
                      const int32_t* fast, int32_t nf, const int32_t* slow, int32_t ns,
                      int64_t ann, orc_summary* out, int32_t nthreads);
+/* The same pool for EMA+OLS and Bollinger grids (S x B row-major columns, params in the
+ * engine's order, include/bt.h). */
+void orc_ema_grid_mt(const int32_t* c, int32_t S, int32_t B, const int32_t* span, int32_t nsp,
+                     const int32_t* ols, int32_t nol, int32_t band_bps, int64_t ann,
+                     orc_summary* out, int32_t nthreads);
+void orc_boll_grid_mt(const int32_t* h, const int32_t* l, const int32_t* c, int32_t S, int32_t B,
+                      const int32_t* win, int32_t nw, const int32_t* k_num, int32_t nk,
+                      int32_t k_den, const int32_t* sl, int32_t nsl, const int32_t* tp,
+                      int32_t ntp, int64_t ann, orc_summary* out, int32_t nthreads);
 
 #ifdef __cplusplus
 }

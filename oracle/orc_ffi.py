@@ -61,7 +61,13 @@ def lib():
                                C.c_int32, C.c_int32, C.c_int64, sp, C.c_void_p, C.c_int32]
         L.orc_sma_grid_mt.argtypes = [i32p, C.c_int32, C.c_int32, i32p, C.c_int32, i32p,
                                       C.c_int32, C.c_int64, sp, C.c_int32]
-        for f in (L.orc_sma, L.orc_ema_ols, L.orc_boll, L.orc_sma_grid_mt):
+        L.orc_ema_grid_mt.argtypes = [i32p, C.c_int32, C.c_int32, i32p, C.c_int32, i32p,
+                                      C.c_int32, C.c_int32, C.c_int64, sp, C.c_int32]
+        L.orc_boll_grid_mt.argtypes = [i32p, i32p, i32p, C.c_int32, C.c_int32, i32p, C.c_int32,
+                                       i32p, C.c_int32, C.c_int32, i32p, C.c_int32, i32p,
+                                       C.c_int32, C.c_int64, sp, C.c_int32]
+        for f in (L.orc_sma, L.orc_ema_ols, L.orc_boll, L.orc_sma_grid_mt, L.orc_ema_grid_mt,
+                  L.orc_boll_grid_mt):
             f.restype = None
         _lib = L
     return _lib
@@ -118,3 +124,23 @@ def sma_grid_mt(closes, fast, slow, ann, nthreads):
     out = np.zeros(S * len(fast) * len(slow), SUMMARY_DTYPE)
     lib().orc_sma_grid_mt(closes, S, B, fast, len(fast), slow, len(slow), ann, out, nthreads)
     return out.reshape(S, len(fast) * len(slow))
+
+
+def ema_grid_mt(closes, span, ols, band_bps, ann, nthreads):
+    closes = np.ascontiguousarray(closes, np.int32)
+    S, B = closes.shape
+    span, ols = (np.ascontiguousarray(x, np.int32) for x in (span, ols))
+    out = np.zeros(S * len(span) * len(ols), SUMMARY_DTYPE)
+    lib().orc_ema_grid_mt(closes, S, B, span, len(span), ols, len(ols), band_bps, ann, out, nthreads)
+    return out.reshape(S, len(span) * len(ols))
+
+
+def boll_grid_mt(highs, lows, closes, win, k_num, k_den, sl, tp, ann, nthreads):
+    h, lo, c = (np.ascontiguousarray(x, np.int32) for x in (highs, lows, closes))
+    S, B = c.shape
+    win, k_num, sl, tp = (np.ascontiguousarray(x, np.int32) for x in (win, k_num, sl, tp))
+    P = len(win) * len(k_num) * len(sl) * len(tp)
+    out = np.zeros(S * P, SUMMARY_DTYPE)
+    lib().orc_boll_grid_mt(h, lo, c, S, B, win, len(win), k_num, len(k_num), k_den, sl, len(sl),
+                           tp, len(tp), ann, out, nthreads)
+    return out.reshape(S, P)

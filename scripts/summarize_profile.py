@@ -27,21 +27,32 @@ line = json.loads([x for x in open(f"{src}/bench.log") if x.startswith("{")][-1]
 kname = line["roofline"]["kernel"].split("::")[-1]
 steps = line["steps"]
 
+# One step launches the strategy kernel once, or, for a bar-split run, the speculative pass,
+# one fix pass per boundary and the combine pass (k_tile.hip): a step's kernel time is the sum
+# of its group of dispatches, the same span the bench line's HIP events bracket.
+def ours(name):
+    return kname in name or "seg_combine" in name
+
+
 rows = list(csv.DictReader(open(glob.glob(f"{src}/trace/*kernel_trace.csv")[0])))
-durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in rows if kname in r["Kernel_Name"]]
-steady = durs[-steps:]
+durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in rows if ours(r["Kernel_Name"])]
+per_step = max(1, len(durs) // (steps + line["warmup"]))
+tail = durs[-steps * per_step:]
+steady = [sum(tail[i:i + per_step]) for i in range(0, len(tail), per_step)]
 stats_csv = glob.glob(f"{src}/trace/*kernel_stats.csv")[0]
 shutil.copy(stats_csv, os.path.join(dst, "kernel_stats.csv"))
 json.dump(line, open(os.path.join(dst, "bench.json"), "w"), indent=1)
 
 
 def pmc(sub):
+    """Per step (the PMC passes run --warmup 1 --steps 3: 4 steps): counters summed over the
+    step's dispatches of our kernels."""
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in glob.glob(f"{src}/{sub}/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            if kname in r["Kernel_Name"]:
+            if ours(r["Kernel_Name"]):
                 agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
-    return {c: sum(d.values()) / len(d) for c, d in agg.items()}
+    return {c: sum(d.values()) / 4 for c, d in agg.items()}
 
 
 c = {}
@@ -53,7 +64,7 @@ write_b = c.get("WRITE_SIZE", 0) * 1024
 alg = line["roofline"]["alg_bytes_per_launch"]
 summary = {
     "command": "python3 bench.py (see bench.json config) under rocprofv3 --kernel-trace --stats",
-    "kernel": kname, "dispatches": len(durs), "steady_dispatches": len(steady),
+    "kernel": kname, "dispatches": len(durs), "dispatches_per_step": per_step, "steady_steps": len(steady),
     "steady_avg_ms": avg_steady_ns / 1e6, "steady_min_ms": min(steady) / 1e6,
     "steady_max_ms": max(steady) / 1e6, "all_dispatch_avg_ms": statistics.mean(durs) / 1e6,
     "bench_ms_per_step": line["ms_per_step"], "bench_kernel_avg_ms": line["roofline"]["kernel_avg_ms"],

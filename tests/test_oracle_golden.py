@@ -196,3 +196,26 @@ def test_biased_reciprocal_floor():
         F = n * W + rem                                  # < 2^43: exact as float64
         got = np.trunc(F.astype(np.float64) * iw).astype(np.int64)
         assert np.array_equal(got, np.broadcast_to(n, got.shape)), "floor key mismatch"
+
+
+def test_threaded_oracle_grids_match_single_calls():
+    """The CPU baseline's pthread pools (orc_ema_grid_mt / orc_boll_grid_mt: one task per symbol,
+    params in the engine's order) give the single-call oracle's summaries."""
+    cols = [F.gen(5, s, 3000, 1) for s in range(3)]
+    g4 = D.config4_grid()
+    out = F.boll_grid_mt(np.stack([x[1] for x in cols]), np.stack([x[2] for x in cols]),
+                         np.stack([x[3] for x in cols]), g4.axes[0], g4.axes[1], 2, g4.axes[2],
+                         g4.axes[3], 98280, 4)
+    for s in range(3):
+        for p in range(0, g4.n_params, 7):
+            kw = g4.param(p)
+            r, _ = F.boll(cols[s][1], cols[s][2], cols[s][3], kw["w"], kw["k_num"], 2, kw["sl"],
+                          kw["tp"], 98280)
+            assert r.tobytes() == out[s, p].tobytes(), (s, p)
+    g3 = D.config3_grid()
+    out = F.ema_grid_mt(np.stack([x[3] for x in cols]), g3.axes[0], g3.axes[1], 20, 98280, 4)
+    for s in range(3):
+        for p in range(g3.n_params):
+            kw = g3.param(p)
+            r, _ = F.ema_ols(cols[s][3], kw["n"], kw["w"], 20, 98280)
+            assert r.tobytes() == out[s, p].tobytes(), (s, p)
