@@ -42,11 +42,12 @@ constexpr int kLH = 6 * kTile + 16;
 constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16, kLhTs = 4 * kTile + 16;
 
 struct TileLds {
-    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, ctr, total;
+    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levf, ctr, total;
 };
 
-// kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks)
-__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb) {
+// kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
+// per side: nsl + ntp)
+__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0) {
     TileLds L{};
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
@@ -60,6 +61,8 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
         L.words = take((size_t)2 * (2 * na * nb + 2 * na) * 8);
         L.win = take((size_t)na * 4);
+        L.lev = take((size_t)2 * 2 * nlev * kTile);  // first-passage bars, [tile & 1][side][level][bar]
+        L.levf = take((size_t)2 * nlev * 8);         // level factors per side
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
@@ -484,6 +487,27 @@ __device__ __forceinline__ void sltp_search(const int32_t* LH, int cur, int32_t 
     xhi = (inH || laH) ? 8 * fH + __builtin_ctz(mH) : kTile;
 }
 
+// First bar in [cur, 63] whose low is <= XL (first_low) or whose high is > XH1 (first_high), 64
+// if none; one lane's search (the level tasks run it with lane = entry bar): the tile suffix
+// decides whether there is a hit at all, then the in-block suffix and the block extrema find its
+// block, then that block's 8 bars.
+__device__ __forceinline__ int first_low(const int32_t* LH, int cur, int32_t XL) {
+    if (cur >= kTile || LH[kLhTs + cur] > XL) return kTile;
+    const int cb = cur >> 3;
+    const uint32_t la = ~gt8(ld4(LH + kLhBx), ld4(LH + kLhBx + 4), XL) & ((0xFEu << cb) & 0xFFu);
+    const int f = LH[kLhSuf + cur] <= XL ? cb : __builtin_ctz(la | 0x100u);
+    const uint32_t m = ~gt8(ld4(LH + 8 * f), ld4(LH + 8 * f + 4), XL) & (f == cb ? (0xFFu << (cur & 7)) & 0xFFu : 0xFFu);
+    return 8 * f + __builtin_ctz(m | 0x100u);
+}
+__device__ __forceinline__ int first_high(const int32_t* LH, int cur, int32_t XH1) {
+    if (cur >= kTile || LH[kLhTs + kTile + cur] <= XH1) return kTile;
+    const int cb = cur >> 3;
+    const uint32_t la = gt8(ld4(LH + kLhBx + 8), ld4(LH + kLhBx + 12), XH1) & ((0xFEu << cb) & 0xFFu);
+    const int f = LH[kLhSuf + kTile + cur] > XH1 ? cb : __builtin_ctz(la | 0x100u);
+    const uint32_t m = gt8(ld4(LH + kTile + 8 * f), ld4(LH + kTile + 8 * f + 4), XH1) & (f == cb ? (0xFFu << (cur & 7)) & 0xFFu : 0xFFu);
+    return 8 * f + __builtin_ctz(m | 0x100u);
+}
+
 // SL/TP levels floor(ce * f / 10000) for 0 < ce < 2^31, 0 < f < 2^15 (spec §4), with the
 // per-lane factor g = fl(f * fl(1e-4)) precomputed: y = fl(ce * g) is within 3 * 2^-53 relative
 // (< 2^-18.7 absolute, y < 2^32.7) of ce * f / 10000 = n + r / 10000 (0 <= r <= 9999), so the
@@ -504,7 +528,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          SegArgs sg, int fix_seg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
-    const TileLds LL = tile_lds_layout(1, R, nw, nk);
+    const int nsl = g.nc, ntp = g.nd, nlev = nsl + ntp;
+    const TileLds LL = tile_lds_layout(1, R, nw, nk, nlev);
     uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);                    // sum c
     unsigned __int128* r2 = reinterpret_cast<unsigned __int128*>(smem + LL.r2);  // sum c^2
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
@@ -514,6 +539,12 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     uint64_t* words = reinterpret_cast<uint64_t*>(smem + LL.words);
     int32_t* win = reinterpret_cast<int32_t*>(smem + LL.win);
     double* kn2d = reinterpret_cast<double*>(smem + LL.ebuf);
+    // SL/TP first passage precomputed per entry bar (level tasks in flags): for every bar b of a
+    // tile and every level the grid uses, the first bar in (b, 63] whose low touches the level
+    // (low side: 1e4 - sl for longs' SL, 1e4 - tp for shorts' TP) or whose high does (high side:
+    // 1e4 + tp, 1e4 + sl), 64 if none; the walk of a trade entered in the tile reads it
+    uint8_t* levt = reinterpret_cast<uint8_t*>(smem + LL.lev);
+    double* levf = reinterpret_cast<double*>(smem + LL.levf);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -538,6 +569,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // level factors (10000 -+ bps) * 1e-4 per side of the trade (level_y)
     const double gl_long = (double)(10000 - sl_bps) * 1e-4, gl_short = (double)(10000 - tp_bps) * 1e-4;
     const double gh_long = (double)(10000 + tp_bps) * 1e-4, gh_short = (double)(10000 + sl_bps) * 1e-4;
+    // this lane's rows of the first-passage tables: long SL / short TP below, long TP / short SL above
+    const int lev_lo_long = isl, lev_lo_short = nsl + itp;
+    const int lev_hi_long = itp, lev_hi_short = ntp + isl;
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
@@ -564,13 +598,19 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
     for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
+    for (int o = tid; o < nlev; o += blockDim.x) {  // the same factors as the walk's (gl_*, gh_*)
+        levf[o] = (double)(10000 - (o < nsl ? g.c[o] : g.d[o - nsl])) * 1e-4;
+        levf[nlev + o] = (double)(10000 + (o < ntp ? g.d[o] : g.c[o - ntp])) * 1e-4;
+    }
+    // condition-word tasks per tile: one per window, then one per side of the level tables
+    const int ntask = nw + 2;
     if (tid == 0) {
         // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
         r1[(T_scan * kTile) % R] = 0;
         r2[(T_scan * kTile) % R] = 0;
         // task rounds are numbered by tile (flags): the counter starts at round T_scan
         const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
-        *ctr = (uint32_t)T_scan * (uint32_t)(nw + ngrab0);
+        *ctr = (uint32_t)T_scan * (uint32_t)(ntask + ngrab0);
     }
     __syncthreads();
 
@@ -645,11 +685,26 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int ptop = ring_pos(T, lane, R);
         const uint64_t P1t = r1[ptop];
         const unsigned __int128 P2t = r2[ptop];
-        const uint32_t base = (uint32_t)T * (uint32_t)(nw + ngrab);
+        const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
-        while (o < (uint32_t)nw) {
+        while (o < (uint32_t)ntask) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
+            if ((int)o >= nw) {  // level task: lane = entry bar b, first passage from b + 1
+                const int side = (int)o - nw;
+                const int32_t* LH = lhs_ + s * kLH;
+                const double cd = (double)c;
+                uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
+#pragma unroll 1
+                for (int i = 0; i < nlev; ++i) {
+                    const double y = level_y(cd, levf[side * nlev + i]);
+                    const int x = side == 0 ? first_low(LH, lane + 1, (int32_t)y)
+                                            : first_high(LH, lane + 1, y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
+                    tab[i * kTile + lane] = (uint8_t)x;
+                }
+                o = grab_value(vn) - base;
+                continue;
+            }
             const int Wn = win[o];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
@@ -770,12 +825,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;
             const uint64_t DP = (W[2 * nw * nk + 2 * iw] & vm) | fb;
             const uint64_t DN = (W[2 * nw * nk + 2 * iw + 1] & vm) | fb;
+            const uint8_t* TL = levt + (k & 1) * 2 * nlev * kTile;  // first-passage tables
+            const uint8_t* TH = TL + nlev * kTile;
             int cur = 0;
             // one trade (entry and/or exit) per call, in bar order; false when the tile is done.
             // Only the first trade of the tile can start open (path carried in a.agg)
             auto trade = [&](auto first_tag) -> bool {
                 constexpr bool FIRST = decltype(first_tag)::value;
                 if (STAMPS) sa.count(3);
+                int xlo = kTile, xhi = kTile;
+                bool entered = false;
                 if (!FIRST || a.pos == 0) {
                     const uint64_t m = (ZL | ZH) & bits_from(cur);
                     if (m == 0) return false;
@@ -783,6 +842,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     const int np = ((ZL >> b) & 1) ? 1 : -1;
                     const int32_t cx = cT[b];
                     const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
+                    // this trade's SL/TP first passages in the tile, read with the entry bar's
+                    // close and returns (one round trip)
+                    xlo = TL[(np > 0 ? lev_lo_long : lev_lo_short) * kTile + b];
+                    xhi = TH[(np > 0 ? lev_hi_long : lev_hi_short) * kTile + b];
+                    entered = true;
                     a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
                     a.ps2 -= q2x;
                     acct_open(a, t0 + b, b, cx);
@@ -796,8 +860,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const bool lg = a.pos > 0;
                 const uint64_t sig = (lg ? DP : DN) & (~0ULL << cur);  // cur < 64 here
                 int x = sig ? __builtin_ctzll(sig) : kTile;
-                int xlo, xhi;
-                sltp_search(LO, cur, XL, XHm1, xlo, xhi);
+                // a position carried into the tile searches with its levels; a trade entered in
+                // it has its first passages from the tables
+                if (FIRST && !entered) sltp_search(LO, cur, XL, XHm1, xlo, xhi);
                 const int xs = min(xlo, xhi);
                 const bool hit = xs < kTile && xs <= x;
                 if (!hit && x >= kTile) return false;
@@ -929,7 +994,7 @@ static int tile_extra_waves(int used, int x) {
 }
 
 size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
-size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g.nb).total; }
+size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd).total; }
 
 int32_t ema_burn_tiles(int32_t max_span) {
     // two fp64 EMA chains from different starts met bit for bit after 131-162 bars (span 10)
