@@ -42,7 +42,7 @@ constexpr int kLH = 6 * kTile + 16;
 constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16, kLhTs = 4 * kTile + 16;
 
 struct TileLds {
-    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levf, ctr, total;
+    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levf, lvb, ctr, total;
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
@@ -63,6 +63,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.win = take((size_t)na * 4);
         L.lev = take((size_t)2 * 2 * nlev * kTile);  // first-passage bars, [tile & 1][side][level][bar]
         L.levf = take((size_t)2 * nlev * 8);         // level factors per side
+        L.lvb = take((size_t)(nlev + 1) * 4);        // distinct SL/TP bps, then their count
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
@@ -425,7 +426,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 //           from an LDS counter (z tests in fp64 with an exact int128 fallback);
 //   parameter waves, tile k: one trade per loop iteration (entry at the first z signal, exit at
 //           the first of SL/TP / signal / forced), O(1) accounting per trade.
-constexpr int kMaxK = 8;             // z thresholds tested per unrolled pass of a window task
+constexpr int kMaxK = 8;
+constexpr int kLevPass = 4;         // SL/TP levels searched together by a level task             // z thresholds tested per unrolled pass of a window task
 
 // 8-bit mask of v_j > X over a (4+4)-int32 group, bit j = element j: the sign bit of X - v_j
 // (no overflow: prices, padding and levels all lie in [0, 2^31)) shifted in by v_alignbit,
@@ -545,6 +547,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // 1e4 + tp, 1e4 + sl), 64 if none; the walk of a trade entered in the tile reads it
     uint8_t* levt = reinterpret_cast<uint8_t*>(smem + LL.lev);
     double* levf = reinterpret_cast<double*>(smem + LL.levf);
+    int32_t* lvb = reinterpret_cast<int32_t*>(smem + LL.lvb);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -569,9 +572,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // level factors (10000 -+ bps) * 1e-4 per side of the trade (level_y)
     const double gl_long = (double)(10000 - sl_bps) * 1e-4, gl_short = (double)(10000 - tp_bps) * 1e-4;
     const double gh_long = (double)(10000 + tp_bps) * 1e-4, gh_short = (double)(10000 + sl_bps) * 1e-4;
-    // this lane's rows of the first-passage tables: long SL / short TP below, long TP / short SL above
-    const int lev_lo_long = isl, lev_lo_short = nsl + itp;
-    const int lev_hi_long = itp, lev_hi_short = ntp + isl;
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
@@ -598,10 +598,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
     for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
-    for (int o = tid; o < nlev; o += blockDim.x) {  // the same factors as the walk's (gl_*, gh_*)
-        levf[o] = (double)(10000 - (o < nsl ? g.c[o] : g.d[o - nsl])) * 1e-4;
-        levf[nlev + o] = (double)(10000 + (o < ntp ? g.d[o] : g.c[o - ntp])) * 1e-4;
-    }
     // condition-word tasks per tile: one per window, then one per side of the level tables
     const int ntask = nw + 2;
     if (tid == 0) {
@@ -611,8 +607,32 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         // task rounds are numbered by tile (flags): the counter starts at round T_scan
         const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
         *ctr = (uint32_t)T_scan * (uint32_t)(ntask + ngrab0);
+        // the distinct SL/TP distances (a level 1e4 -+ bps is shared by every SL and TP of that
+        // bps: config 4's {50, 100} and {50, 100, 200, 400} make 4 levels per side, not 6) and
+        // their factors, the same as the walk's (gl_*, gh_*)
+        int nu = 0;
+        for (int o = 0; o < nlev; ++o) {
+            const int32_t v = o < nsl ? g.c[o] : g.d[o - nsl];
+            bool seen = false;
+            for (int u = 0; u < nu; ++u) seen |= lvb[u] == v;
+            if (!seen) {
+                levf[nu] = (double)(10000 - v) * 1e-4;
+                levf[nlev + nu] = (double)(10000 + v) * 1e-4;
+                lvb[nu++] = v;
+            }
+        }
+        lvb[nlev] = nu;
     }
     __syncthreads();
+    const int nu = lvb[nlev];
+    // this lane's rows of the first-passage tables: long SL / short TP below (1e4 - bps), long
+    // TP / short SL above (1e4 + bps)
+    int usl = 0, utp = 0;
+    for (int u = 0; u < nu; ++u) {
+        usl = lvb[u] == sl_bps ? u : usl;
+        utp = lvb[u] == tp_bps ? u : utp;
+    }
+    const int lev_lo_long = usl, lev_lo_short = utp, lev_hi_long = utp, lev_hi_short = usl;
 
     TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     unsigned __int128 cy2 = 0;
@@ -695,12 +715,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const int32_t* LH = lhs_ + s * kLH;
                 const double cd = (double)c;
                 uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
+                // kLevPass levels per pass: independent searches, all stored after all
 #pragma unroll 1
-                for (int i = 0; i < nlev; ++i) {
-                    const double y = level_y(cd, levf[side * nlev + i]);
-                    const int x = side == 0 ? first_low(LH, lane + 1, (int32_t)y)
-                                            : first_high(LH, lane + 1, y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
-                    tab[i * kTile + lane] = (uint8_t)x;
+                for (int i = 0; i < nu; i += kLevPass) {
+                    int x[kLevPass];
+#pragma unroll
+                    for (int u = 0; u < kLevPass; ++u) {
+                        const double y = level_y(cd, levf[side * nlev + min(i + u, nu - 1)]);
+                        x[u] = side == 0 ? first_low(LH, lane + 1, (int32_t)y)
+                                         : first_high(LH, lane + 1, y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kLevPass; ++u) tab[min(i + u, nu - 1) * kTile + lane] = (uint8_t)x[u];
                 }
                 o = grab_value(vn) - base;
                 continue;

@@ -87,16 +87,13 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
     a.agg = kAggId;
 }
 
-// Close the open trade at global bar t for price px; `st` aggregates the trade's whole price
-// path in order, exit point included.
+// Close the open trade (a.pos, a.e, a.ce) at global bar t for price px, given the trade's
+// adverse / favourable excursions lo / hi and internal drawdown `path` (all relative to the
+// entry close, in the trade's direction), its pnl and its hash term mix(w).
 template <bool PARITY, bool SEG = false>
-__device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
-                                           bt_trade* tr, int cap) {
-    const bool lg = a.pos > 0;
-    const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;  // |.| < 2^31
-    const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
-    const int32_t path = lg ? st.dd : st.du;
-    const int32_t pnl = lg ? px - a.ce : a.ce - px;
+__device__ __forceinline__ void acct_fold(TradeAcct& a, int t, int32_t px, int32_t lo, int32_t hi,
+                                          int32_t path, int32_t pnl, uint64_t mix, bt_trade* tr,
+                                          int cap) {
     if (SEG) {
         const int64_t A0 = a.A, B0 = a.Bq;
         a.C = max(a.C, A0 - (int64_t)lo);
@@ -109,9 +106,7 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, cons
     }
     a.R += pnl;
     a.expo += t - a.e;
-    const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
-                       ((uint64_t)lg << 62);
-    a.h += trade_mix(w);
+    a.h += mix;
     if (PARITY && a.ntr < cap) {
         bt_trade r;
         r.entry_bar = a.e;
@@ -123,6 +118,24 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, cons
         tr[a.ntr] = r;
     }
     a.ntr++;
+}
+
+// Hash term of a trade (spec §4): w = entry | exit << 31 | (side > 0) << 62.
+__device__ __forceinline__ uint64_t trade_term(int e, int t, bool lg) {
+    return trade_mix((uint64_t)(uint32_t)e | ((uint64_t)(uint32_t)t << 31) | ((uint64_t)lg << 62));
+}
+
+// Close the open trade at global bar t for price px; `st` aggregates the trade's whole price
+// path in order, exit point included.
+template <bool PARITY, bool SEG = false>
+__device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
+                                           bt_trade* tr, int cap) {
+    const bool lg = a.pos > 0;
+    const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;  // |.| < 2^31
+    const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
+    const int32_t path = lg ? st.dd : st.du;
+    const int32_t pnl = lg ? px - a.ce : a.ce - px;
+    acct_fold<PARITY, SEG>(a, t, px, lo, hi, path, pnl, trade_term(a.e, t, lg), tr, cap);
 }
 
 __device__ __forceinline__ void acct_open(TradeAcct& a, int t, int b, int32_t px) {
