@@ -419,15 +419,22 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 }
 
 // ----------------------------------------------------------------------------- Bollinger
-// Workgroup = parameter waves + one helper wave, one barrier per tile:
+// Workgroup = parameter waves + one helper wave + task-only waves, one barrier per tile:
 //   helper, tile k+2: closes/highs/lows -> returns, drawdown sparse table, prefix rings, the raw
-//           lows/highs and their 8-bar block minima/maxima (SL/TP first-passage search);
-//   every wave, tile k+1, after its own work: condition words, one task per window grabbed
-//           from an LDS counter (z tests in fp64 with an exact int128 fallback);
+//           lows/highs and their 8-bar block / in-block / tile suffix extrema;
+//   every wave, tile k+1, after its own work: tasks grabbed from an LDS counter — per window the
+//           condition words (z tests in fp64 with an exact int128 fallback), per side the SL/TP
+//           first-passage tables of the tile's entry bars;
 //   parameter waves, tile k: one trade per loop iteration (entry at the first z signal, exit at
 //           the first of SL/TP / signal / forced), O(1) accounting per trade.
-constexpr int kMaxK = 8;
-constexpr int kLevPass = 4;         // SL/TP levels searched together by a level task             // z thresholds tested per unrolled pass of a window task
+constexpr int kMaxK = 8;             // z thresholds tested per unrolled pass of a window task
+// SL/TP levels per level task (searched together); 1, 2 or 4 levels per task and level tasks
+// queued before the window tasks measured within noise or slower (config 4: 7.91-8.06 ms)
+constexpr int kLevPassLog = 1, kLevPass = 1 << kLevPassLog;
+// Parameter waves take tasks after their walk too: with the level tables the tasks, not the walk,
+// set the tile time (config 4 at 500 symbols: task waves ~11.6k busy cycles per tile, parameter
+// waves ~6.1k busy and ~6.5k at the barrier; 8.51 -> 7.96 ms)
+constexpr bool kWalkOnly = false;
 
 // 8-bit mask of v_j > X over a (4+4)-int32 group, bit j = element j: the sign bit of X - v_j
 // (no overflow: prices, padding and levels all lie in [0, 2^31)) shifted in by v_alignbit,
@@ -598,15 +605,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     for (int o = tid; o < nw; o += blockDim.x) win[o] = g.a[o];
     for (int o = tid; o < nk; o += blockDim.x) kn2d[o] = (double)((int64_t)g.b[o] * g.b[o]);
-    // condition-word tasks per tile: one per window, then one per side of the level tables
-    const int ntask = nw + 2;
+    // tasks per tile: one per window (condition words), then per side one per kLevPass levels
+    // (first-passage tables)
+    auto task_count = [&](int nu) { return nw + 2 * ((nu + kLevPass - 1) / kLevPass); };
     if (tid == 0) {
         // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
         r1[(T_scan * kTile) % R] = 0;
         r2[(T_scan * kTile) % R] = 0;
-        // task rounds are numbered by tile (flags): the counter starts at round T_scan
-        const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
-        *ctr = (uint32_t)T_scan * (uint32_t)(ntask + ngrab0);
         // the distinct SL/TP distances (a level 1e4 -+ bps is shared by every SL and TP of that
         // bps: config 4's {50, 100} and {50, 100, 200, 400} make 4 levels per side, not 6) and
         // their factors, the same as the walk's (gl_*, gh_*)
@@ -622,9 +627,12 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             }
         }
         lvb[nlev] = nu;
+        // task rounds are numbered by tile (flags): the counter starts at round T_scan
+        const int ngrab0 = nwaves - (kWalkOnly && nextra >= 2 ? npw : 0);
+        *ctr = (uint32_t)T_scan * (uint32_t)(task_count(nu) + ngrab0);
     }
     __syncthreads();
-    const int nu = lvb[nlev];
+    const int nu = lvb[nlev], ntask = task_count(nu);
     // this lane's rows of the first-passage tables: long SL / short TP below (1e4 - bps), long
     // TP / short SL above (1e4 + bps)
     int usl = 0, utp = 0;
@@ -692,7 +700,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     };
 
     // with two or more task-only waves the parameter waves only walk (at raised priority)
-    const bool walk_only = nextra >= 2;
+    const bool walk_only = kWalkOnly && nextra >= 2;
     const bool no_tasks = walk_only && wave < npw;
     const int ngrab = nwaves - (walk_only ? npw : 0);
 
@@ -710,14 +718,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 #pragma unroll 1
         while (o < (uint32_t)ntask) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
-            if ((int)o >= nw) {  // level task: lane = entry bar b, first passage from b + 1
-                const int side = (int)o - nw;
+            const int ow = (int)o, ol = ow - nw;  // window task ow, or level task ol
+            if (ol >= 0) {  // level task: lane = entry bar b, first passage from b + 1
+                const int side = ol & 1, i = ol >> 1 << kLevPassLog;
                 const int32_t* LH = lhs_ + s * kLH;
                 const double cd = (double)c;
                 uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
-                // kLevPass levels per pass: independent searches, all stored after all
-#pragma unroll 1
-                for (int i = 0; i < nu; i += kLevPass) {
+                // kLevPass levels: independent searches, all stored after all
+                {
                     int x[kLevPass];
 #pragma unroll
                     for (int u = 0; u < kLevPass; ++u) {
@@ -731,7 +739,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 o = grab_value(vn) - base;
                 continue;
             }
-            const int Wn = win[o];
+            const int Wn = win[ow];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
             const int pj = ring_back(ptop, Wn, R);
@@ -762,15 +770,15 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const uint64_t zl = __ballot(valid && big && Dv < 0);
                 const uint64_t zh = __ballot(valid && big && Dv > 0);
                 if (lane == 0) {
-                    Wd[2 * ((int)o * nk + q)] = zl;
-                    Wd[2 * ((int)o * nk + q) + 1] = zh;
+                    Wd[2 * (ow * nk + q)] = zl;
+                    Wd[2 * (ow * nk + q) + 1] = zh;
                 }
             }
             }
             const uint64_t dp = __ballot(valid && Dv >= 0), dn = __ballot(valid && Dv <= 0);
             if (lane == 0) {
-                Wd[2 * nw * nk + 2 * o] = dp;
-                Wd[2 * nw * nk + 2 * o + 1] = dn;
+                Wd[2 * nw * nk + 2 * ow] = dp;
+                Wd[2 * nw * nk + 2 * ow + 1] = dn;
             }
             o = grab_value(vn) - base;
         }
