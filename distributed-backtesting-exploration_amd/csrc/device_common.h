@@ -96,6 +96,45 @@ __device__ __forceinline__ int64_t wave_iscan_i64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// ---- cross-lane moves without LDS (DPP / readlane; ds_bpermute costs an LDS round trip)
+// DPP controls: quad_perm [p0 p1 p2 p3] = p0 | p1 << 2 | p2 << 4 | p3 << 6; row_shl:d = 0x100 + d;
+// row_mirror 0x140; row_half_mirror 0x141 (lane i <-> 7 - i in each 8); row_newbcast:k = 0x150 + k
+// (lane k of each 16-lane row to the whole row, gfx90a+). Lanes whose source falls outside the
+// row keep `old`.
+// The result is pinned where it is computed: a DPP move sunk into a divergent branch would read
+// source lanes that EXEC has switched off there (and get `old`).
+template <int CTRL>
+__device__ __forceinline__ int32_t dpp(int32_t old, int32_t x) {
+    int32_t r = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)old, (uint32_t)x, CTRL, 0xf, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
+// Partner value of the disjoint-sparse-table build at level m (group of 2^m lanes): a lane in
+// the left half of its group reads the group's last lane, a lane in the right half its first.
+template <int M>
+__device__ __forceinline__ int32_t dst_partner(int32_t x, int lane) {
+    if constexpr (M == 1) {
+        return dpp<0xB1>(0, x);                                   // quad_perm [1 0 3 2]
+    } else if constexpr (M == 2) {
+        return dpp<0x0F>(0, x);                                   // quad_perm [3 3 0 0]
+    } else if constexpr (M == 3) {
+        const int32_t hm = dpp<0x141>(0, x);                      // i <-> 7 - i
+        const int32_t q3 = dpp<0xFF>(0, hm), q0 = dpp<0x00>(0, hm);  // quad lane 3 / quad lane 0
+        return (lane & 4) ? q3 : q0;
+    } else if constexpr (M == 4) {
+        const int32_t r0 = dpp<0x150>(0, x), r15 = dpp<0x15F>(0, x);  // row lane 0 / row lane 15
+        return (lane & 8) ? r0 : r15;
+    } else {
+        static_assert(M == 5, "six levels for 64-lane tiles");
+        const int32_t l0 = (int32_t)__builtin_amdgcn_readlane((uint32_t)x, 0);
+        const int32_t l31 = (int32_t)__builtin_amdgcn_readlane((uint32_t)x, 31);
+        const int32_t l32 = (int32_t)__builtin_amdgcn_readlane((uint32_t)x, 32);
+        const int32_t l63 = (int32_t)__builtin_amdgcn_readlane((uint32_t)x, 63);
+        return (lane & 16) ? ((lane & 32) ? l32 : l0) : ((lane & 32) ? l63 : l31);
+    }
+}
+
 // Value of lane 63 as a wave-uniform (SGPR) int64.
 __device__ __forceinline__ int64_t lane63_i64(int64_t x) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, 63);

@@ -663,37 +663,55 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         int32_t* LH = lhs_ + s * kLH;
         LH[lane] = lv;
         LH[kTile + lane] = hv;
+        // 8-bar block extrema: xor 1, xor 2 inside quads, then the other quad of the 8
         int32_t mn = lv, mx = hv;
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1) {
-            mn = min(mn, __shfl_xor(mn, d, 64));
-            mx = max(mx, __shfl_xor(mx, d, 64));
-        }
+        mn = min(mn, dpp<0xB1>(0, mn));
+        mx = max(mx, dpp<0xB1>(0, mx));
+        mn = min(mn, dpp<0x4E>(0, mn));
+        mx = max(mx, dpp<0x4E>(0, mx));
+        mn = min(mn, dpp<0x141>(0, mn));
+        mx = max(mx, dpp<0x141>(0, mx));
         if ((lane & 7) == 0) {
             LH[kLhBx + (lane >> 3)] = mn;
             LH[kLhBx + 8 + (lane >> 3)] = mx;
         }
-        // min low / max high from each bar to the end of its 8-bar block (suffix within the block)
+        // min low / max high from each bar to the end of its 8-bar block (suffix within the
+        // block: row_shl, masked at the block end) ...
         int32_t smn = lv, smx = hv;
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1) {
-            const int32_t on = __shfl_down(smn, d, 64), ox = __shfl_down(smx, d, 64);
-            if ((lane & 7) + d < 8) {
-                smn = min(smn, on);
-                smx = max(smx, ox);
-            }
-        }
+        auto blk = [&](auto dtag) {
+            constexpr int d = decltype(dtag)::value;
+            const int32_t on = dpp<0x100 + d>(INT32_MAX, smn), ox = dpp<0x100 + d>(INT32_MIN, smx);
+            const bool in = (lane & 7) + d < 8;
+            smn = in ? min(smn, on) : smn;
+            smx = in ? max(smx, ox) : smx;
+        };
+        blk(std::integral_constant<int, 1>{});
+        blk(std::integral_constant<int, 2>{});
+        blk(std::integral_constant<int, 4>{});
         LH[kLhSuf + lane] = smn;
         LH[kLhSuf + kTile + lane] = smx;
-        // ... and to the end of the tile (one test tells whether a level is touched at all)
+        // ... and to the end of the tile (one test tells whether a level is touched at all): in
+        // each 16-lane row by row_shl, then the later rows' totals (their lane 0) by readlane
         int32_t tmn = lv, tmx = hv;
-#pragma unroll
-        for (int d = 1; d < kTile; d <<= 1) {
-            const int32_t on = __shfl_down(tmn, d, 64), ox = __shfl_down(tmx, d, 64);
-            if (lane + d < kTile) {
-                tmn = min(tmn, on);
-                tmx = max(tmx, ox);
-            }
+        auto row = [&](auto dtag) {
+            constexpr int d = decltype(dtag)::value;
+            tmn = min(tmn, dpp<0x100 + d>(INT32_MAX, tmn));
+            tmx = max(tmx, dpp<0x100 + d>(INT32_MIN, tmx));
+        };
+        row(std::integral_constant<int, 1>{});
+        row(std::integral_constant<int, 2>{});
+        row(std::integral_constant<int, 4>{});
+        row(std::integral_constant<int, 8>{});
+        {
+            const int32_t n3 = (int32_t)__builtin_amdgcn_readlane((uint32_t)tmn, 48);
+            const int32_t n2 = min((int32_t)__builtin_amdgcn_readlane((uint32_t)tmn, 32), n3);
+            const int32_t n1 = min((int32_t)__builtin_amdgcn_readlane((uint32_t)tmn, 16), n2);
+            const int32_t x3 = (int32_t)__builtin_amdgcn_readlane((uint32_t)tmx, 48);
+            const int32_t x2 = max((int32_t)__builtin_amdgcn_readlane((uint32_t)tmx, 32), x3);
+            const int32_t x1 = max((int32_t)__builtin_amdgcn_readlane((uint32_t)tmx, 16), x2);
+            const int r = lane >> 4;
+            tmn = min(tmn, r == 0 ? n1 : r == 1 ? n2 : r == 2 ? n3 : INT32_MAX);
+            tmx = max(tmx, r == 0 ? x1 : r == 1 ? x2 : r == 2 ? x3 : INT32_MIN);
         }
         LH[kLhTs + lane] = tmn;
         LH[kLhTs + kTile + lane] = tmx;
@@ -830,7 +848,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     for (int k = T_scan; k < T_end; ++k) {
         const int t0 = k * kTile;
         if (helper && k + 2 < T_end) {
+#if BT_HELPER_PRIO
+            __builtin_amdgcn_s_setprio(3);
+#endif
             scan(k + 2, cpre, hpre, lpre);
+#if BT_HELPER_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             const int tn = t0 + 3 * kTile + lane;
             cpre = ldc(crow, B, tn, 0);
             hpre = ldc(hrow, B, tn, 0);

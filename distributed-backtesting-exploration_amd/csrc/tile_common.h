@@ -2,16 +2,19 @@
 // the per-tile close scan (returns, drawdown sparse table) and the per-lane trade accounting
 // that runs only at position changes. Spec: docs/oracle_spec.md §3-§4.
 #pragma once
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace bt {
 
 constexpr int kTileStages = 3;  // tile buffers in flight: scanned (k+2), flagged (k+1), walked (k)
 
-// Wave-wide shuffle of an Agg from lane `src`.
-__device__ __forceinline__ Agg tile_shfl_agg(const Agg& a, int src) {
-    return Agg{__shfl(a.mx, src, 64), __shfl(a.mn, src, 64), __shfl(a.dd, src, 64),
-               __shfl(a.du, src, 64)};
+// The Agg of the level-M partner lane (dst_partner).
+template <int M>
+__device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
+    return Agg{dst_partner<M>(a.mx, lane), dst_partner<M>(a.mn, lane), dst_partner<M>(a.dd, lane),
+               dst_partner<M>(a.du, lane)};
 }
 
 struct TileCarry {
@@ -40,17 +43,23 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
     Agg S = agg_one(c), Pp = S;
     D[lane] = S;
-#pragma unroll
-    for (int m = 1; m < kDstLevels; ++m) {
-        const int half = 1 << (m - 1);
-        const bool left = (lane & half) == 0;
-        const Agg expose = agg_sel(left, S, Pp);
-        const int src = left ? (lane | (2 * half - 1)) : (lane & ~(2 * half - 1));
-        const Agg part = tile_shfl_agg(expose, src);
+    // level m: a lane in the left half of its 2^m group merges the right half (exposed as the
+    // group's last lane's prefix) into its suffix, a right-half lane the left half (the first
+    // lane's suffix) into its prefix; partners move by DPP / readlane, no LDS round trip
+    auto level = [&](auto mtag) {
+        constexpr int m = decltype(mtag)::value;
+        const bool left = (lane & (1 << (m - 1))) == 0;
+        const Agg part = dst_partner_agg<m>(agg_sel(left, S, Pp), lane);
         S = agg_sel(left, agg_merge(S, part), S);
         Pp = agg_sel(left, Pp, agg_merge(part, Pp));
         D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
-    }
+    };
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 3>{});
+    level(std::integral_constant<int, 4>{});
+    level(std::integral_constant<int, 5>{});
+    static_assert(kDstLevels == 6, "levels 1..5 above");
     return pre;
 }
 
