@@ -1,5 +1,7 @@
 // device_common.h — device helpers shared by the strategy kernels.
 #pragma once
+#include <type_traits>
+
 #include "internal.h"
 
 namespace bt {
@@ -133,6 +135,38 @@ __device__ __forceinline__ int32_t dst_partner(int32_t x, int lane) {
         const int32_t l63 = (int32_t)__builtin_amdgcn_readlane((uint32_t)x, 63);
         return (lane & 16) ? ((lane & 32) ? l32 : l0) : ((lane & 32) ? l63 : l31);
     }
+}
+
+// The Agg of the level-M partner lane (dst_partner).
+template <int M>
+__device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
+    return Agg{dst_partner<M>(a.mx, lane), dst_partner<M>(a.mn, lane), dst_partner<M>(a.dd, lane),
+               dst_partner<M>(a.du, lane)};
+}
+
+// Disjoint sparse table of one 64-bar tile, one whole wave (lane = bar, c = its close): level 0
+// the bar itself; level m = 1..5 the aggregate from the bar to the end of its half of the
+// aligned 2^(m+1) block (left halves) or from the half's start to the bar (right halves).
+// Doubling: at level m a lane in the left half of its 2^m group merges the right half (exposed
+// as the group's last lane's prefix) into its suffix S, a right-half lane the left half (the
+// first lane's suffix) into its prefix Pp; partners move by DPP / readlane, no LDS round trip.
+__device__ __forceinline__ void dst_build(int32_t c, int lane, Agg* D) {
+    Agg S = agg_one(c), Pp = S;
+    D[lane] = S;
+    auto level = [&](auto mtag) {
+        constexpr int m = decltype(mtag)::value;
+        const bool left = (lane & (1 << (m - 1))) == 0;
+        const Agg part = dst_partner_agg<m>(agg_sel(left, S, Pp), lane);
+        S = agg_sel(left, agg_merge(S, part), S);
+        Pp = agg_sel(left, Pp, agg_merge(part, Pp));
+        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
+    };
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 3>{});
+    level(std::integral_constant<int, 4>{});
+    level(std::integral_constant<int, 5>{});
+    static_assert(kDstLevels == 6, "levels 1..5 above");
 }
 
 // Value of lane 63 as a wave-uniform (SGPR) int64.

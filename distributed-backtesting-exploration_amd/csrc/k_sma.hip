@@ -56,12 +56,6 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     return L;
 }
 
-// Wave-wide shuffle of an Agg from lane `src`.
-__device__ __forceinline__ Agg shfl_agg(const Agg& a, int src) {
-    return Agg{__shfl(a.mx, src, 64), __shfl(a.mn, src, 64), __shfl(a.dd, src, 64),
-               __shfl(a.du, src, 64)};
-}
-
 // Stage 1 for one tile, executed by one whole wave (lane = bar of the tile).
 struct ScanCarry {
     int64_t P;          // sum of closes before the tile
@@ -94,25 +88,8 @@ __device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, i
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
 }
 
-// DST by doubling: S_m / P_m = aggregate from the bar to the end / from the start of its
-// aligned 2^m block. Level L of the DST is S_L on left halves and P_L on right halves.
-__device__ __forceinline__ void stage_dst(int32_t c, int lane, Agg* D) {
-    Agg S = agg_one(c), Pp = S;
-    D[lane] = S;  // level 0
-#pragma unroll
-    for (int m = 1; m < kDstLevels; ++m) {
-        const int half = 1 << (m - 1);
-        const bool left = (lane & half) == 0;
-        // each lane exposes what its partner needs: right-half lanes their prefix, left-half
-        // lanes their suffix; left lanes read the block end, right lanes the block start
-        const Agg expose = agg_sel(left, S, Pp);
-        const int src = left ? (lane | (2 * half - 1)) : (lane & ~(2 * half - 1));
-        const Agg part = shfl_agg(expose, src);
-        S = agg_sel(left, agg_merge(S, part), S);
-        Pp = agg_sel(left, Pp, agg_merge(part, Pp));
-        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
-    }
-}
+// The tile's drawdown table (device_common.h dst_build), from this wave's copy of the closes.
+__device__ __forceinline__ void stage_dst(int32_t c, int lane, Agg* D) { dst_build(c, lane, D); }
 
 // Stage 2 for one tile: int32 floor keys for every window. lane = bar, so the window length
 // and its reciprocal are wave-uniform and the top of the ring is read once per tile.

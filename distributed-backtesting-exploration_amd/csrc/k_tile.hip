@@ -848,13 +848,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     for (int k = T_scan; k < T_end; ++k) {
         const int t0 = k * kTile;
         if (helper && k + 2 < T_end) {
-#if BT_HELPER_PRIO
-            __builtin_amdgcn_s_setprio(3);
-#endif
             scan(k + 2, cpre, hpre, lpre);
-#if BT_HELPER_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
             const int tn = t0 + 3 * kTile + lane;
             cpre = ldc(crow, B, tn, 0);
             hpre = ldc(hrow, B, tn, 0);

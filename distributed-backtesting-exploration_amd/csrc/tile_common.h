@@ -2,20 +2,12 @@
 // the per-tile close scan (returns, drawdown sparse table) and the per-lane trade accounting
 // that runs only at position changes. Spec: docs/oracle_spec.md §3-§4.
 #pragma once
-#include <type_traits>
-
 #include "device_common.h"
 
 namespace bt {
 
 constexpr int kTileStages = 3;  // tile buffers in flight: scanned (k+2), flagged (k+1), walked (k)
 
-// The Agg of the level-M partner lane (dst_partner).
-template <int M>
-__device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
-    return Agg{dst_partner<M>(a.mx, lane), dst_partner<M>(a.mn, lane), dst_partner<M>(a.dd, lane),
-               dst_partner<M>(a.du, lane)};
-}
 
 struct TileCarry {
     int64_t P;       // sum of closes before the tile
@@ -41,25 +33,7 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     ql[kTile + lane] = wave_iscan_i64(q2);
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
-    Agg S = agg_one(c), Pp = S;
-    D[lane] = S;
-    // level m: a lane in the left half of its 2^m group merges the right half (exposed as the
-    // group's last lane's prefix) into its suffix, a right-half lane the left half (the first
-    // lane's suffix) into its prefix; partners move by DPP / readlane, no LDS round trip
-    auto level = [&](auto mtag) {
-        constexpr int m = decltype(mtag)::value;
-        const bool left = (lane & (1 << (m - 1))) == 0;
-        const Agg part = dst_partner_agg<m>(agg_sel(left, S, Pp), lane);
-        S = agg_sel(left, agg_merge(S, part), S);
-        Pp = agg_sel(left, Pp, agg_merge(part, Pp));
-        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
-    };
-    level(std::integral_constant<int, 1>{});
-    level(std::integral_constant<int, 2>{});
-    level(std::integral_constant<int, 3>{});
-    level(std::integral_constant<int, 4>{});
-    level(std::integral_constant<int, 5>{});
-    static_assert(kDstLevels == 6, "levels 1..5 above");
+    dst_build(c, lane, D);
     return pre;
 }
 

@@ -33,7 +33,7 @@ import threading
 import time
 import uuid
 from concurrent import futures
-from typing import Dict, List, Optional
+from typing import Dict, List, NamedTuple, Optional
 
 import grpc
 
@@ -44,6 +44,24 @@ log = logging.getLogger("dbx_amd.dispatcher")
 DEFAULT_RECEIVE = 4 * 1024 * 1024   # grpcio's (and tonic's) default client receive limit
 REPLY_MARGIN = 64 * 1024            # JobsReply framing beyond the payload bytes
 JOB_OVERHEAD = 64                   # per Job: UUID string, field tags and lengths
+
+
+class Job(NamedTuple):  # a JobsReply entry before serialization
+    id: str
+    File: bytes
+
+
+class Reply:
+    """A JobsReply as (id, File) pairs, serialized straight to wire bytes by
+    proto.encode_jobs_reply: building protobuf messages first would copy every payload twice
+    more (the message runtime moves ~1 GB/s, a join several)."""
+    __slots__ = ("jobs",)
+
+    def __init__(self, jobs: List[Job]):
+        self.jobs = jobs
+
+    def SerializeToString(self) -> bytes:
+        return P.encode_jobs_reply(self.jobs)
 
 
 def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
@@ -198,13 +216,13 @@ class Dispatcher:
             with self.done_lock:
                 self.job_paths[jid] = path
                 self.inflight[jid] = (ctx.peer(), path)
-            jobs.append(P.Job(id=jid, File=data))
+            jobs.append(Job(jid, data))
         log.info("Num files to run: %d", len(jobs))
-        return P.JobsReply(jobs=jobs)
+        return Reply(jobs)
 
 
 def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 << 20,
-          gzip: bool = True):
+          gzip: bool = True, threads: int = 16):
     dispatcher.max_reply_bytes = min(dispatcher.max_reply_bytes, max_send - REPLY_MARGIN)
     ser = lambda m: m.SerializeToString()  # noqa: E731
     handlers = {
@@ -218,7 +236,7 @@ def serve(dispatcher: Dispatcher, addr: str = "[::1]:50051", max_send: int = 64 
             dispatcher.request_jobs, request_deserializer=P.JobsRequest.FromString,
             response_serializer=ser),
     }
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=8),
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=threads),
                          compression=grpc.Compression.Gzip if gzip else grpc.Compression.NoCompression,
                          options=[("grpc.max_send_message_length", max_send)])
     server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(P.SERVICE, handlers),))

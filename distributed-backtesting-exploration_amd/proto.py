@@ -77,3 +77,26 @@ MAX_RECEIVE_KEY = "x-dbx-max-receive"
 
 def method_path(name: str) -> str:
     return f"/{SERVICE}/{name}"
+
+
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def encode_jobs_reply(jobs) -> bytes:
+    """Wire bytes of JobsReply{jobs: [Job{id, File}]} for (id, file_bytes) pairs, identical to
+    JobsReply(...).SerializeToString() (proto3: empty fields omitted, fields in number order),
+    built with one join: the payload bytes are copied once, not into message objects first."""
+    parts = []
+    for jid, data in jobs:
+        idb = jid.encode("utf-8")
+        head = (b"\x0a" + _varint(len(idb)) if idb else b"")
+        fhead = (b"\x12" + _varint(len(data)) if data else b"")
+        parts.append(b"\x0a" + _varint(len(head) + len(idb) + len(fhead) + len(data)))
+        parts += [head, idb, fhead, data]
+    return b"".join(parts)

@@ -37,6 +37,13 @@ CONNECTED = threading.Event()   # main.rs:25
 Processor = Callable[[Sequence[tuple]], Sequence[str]]
 
 
+class _Merged:  # JobsReplies merged into one engine batch (worker-side batching)
+    __slots__ = ("jobs",)
+
+    def __init__(self, jobs):
+        self.jobs = jobs
+
+
 def engine_processor(engine) -> Processor:
     def run(jobs):
         return [data for _status, data in engine.run_batch(jobs)]
@@ -73,7 +80,8 @@ class Worker:
     def __init__(self, target: str, processor: Processor, cores: Optional[int] = None,
                  job_tick: float = 0.250, status_tick: float = 1.0,
                  max_receive: int = 4 * 1024 * 1024, max_batch_bytes: int = 0,
-                 min_batch_jobs: int = 0, linger_s: float = 0.2):
+                 min_batch_jobs: int = 0, linger_s: float = 0.2, fetchers: int = 1,
+                 max_queued_bytes: int = 0):
         self.target = target
         self.processor = processor
         # handlers.rs:35 reports num_cpus/2; a GPU worker reports its batch capacity instead
@@ -91,8 +99,15 @@ class Worker:
         # `min_batch_jobs` symbols (a launch runs one workgroup per symbol: hundreds fill it)
         self.min_batch_jobs, self.linger_s = min_batch_jobs, linger_s
         self.max_receive = max_receive
-        opts = [("grpc.max_receive_message_length", max_receive)]
-        self.channel = grpc.insecure_channel(target, options=opts)
+        # extra fetchers: threads with their own channels (TCP connections) that keep RequestJobs
+        # in flight beside the job tick, while fewer than `max_queued_bytes` of replies wait for
+        # the compute thread: one grpcio channel moves ~1 GB/s, the engine ingests 100+ GB/s
+        self.fetchers = max(1, fetchers)
+        self.max_queued_bytes = max_queued_bytes or max(4 * max_batch_bytes, 1 << 30)
+        self._queued = 0
+        self._qlock = threading.Lock()
+        self._opts = [("grpc.max_receive_message_length", max_receive)]
+        self.channel = grpc.insecure_channel(target, options=self._opts)
         u = self.channel.unary_unary
         ser = lambda m: m.SerializeToString()  # noqa: E731
         self._status = u(P.method_path("SendStatus"), request_serializer=ser,
@@ -102,27 +117,59 @@ class Worker:
         self._complete = u(P.method_path("CompleteJob"), request_serializer=ser,
                            response_deserializer=P.CompleteReply.FromString)
 
+    def _put(self, reply):
+        with self._qlock:
+            self._queued += sum(len(j.File) for j in reply.jobs)
+        self.reply_q.put(reply)
+
+    def _take(self, timeout=None):
+        reply = self.reply_q.get(timeout=timeout) if timeout is not None else self.reply_q.get_nowait()
+        with self._qlock:
+            self._queued -= sum(len(j.File) for j in reply.jobs)
+        return reply
+
+    def _fetch(self, idx):
+        """Extra fetcher `idx` >= 1: RequestJobs on its own connection while the queue has room."""
+        ch = grpc.insecure_channel(self.target, options=self._opts + [
+            ("grpc.use_local_subchannel_pool", 1), ("dbx.fetcher", idx)])
+        req = ch.unary_unary(P.method_path("RequestJobs"), request_serializer=lambda m: m.SerializeToString(),
+                             response_deserializer=P.JobsReply.FromString)
+        try:
+            while not self.stop.is_set():
+                with self._qlock:
+                    full = self._queued >= self.max_queued_bytes
+                if full:
+                    time.sleep(self.job_tick)
+                    continue
+                try:
+                    reply = req(P.JobsRequest(cores=self.cores),
+                                metadata=((P.MAX_RECEIVE_KEY, str(self.max_receive)),))
+                except grpc.RpcError:  # empty queue / server gone
+                    time.sleep(self.job_tick)
+                    continue
+                self._put(reply)
+        finally:
+            ch.close()
+
     # main.rs:38-42 — the compute OS thread
     def _compute(self):
         while not self.stop.is_set():
             try:
-                reply = self.reply_q.get(timeout=0.05)
+                reply = self._take(timeout=0.05)
             except queue.Empty:
                 continue
             if self.max_batch_bytes > 0:
-                size = sum(len(j.File) for j in reply.jobs)
-                merged = P.JobsReply(jobs=list(reply.jobs))
+                # the replies' Job messages by reference (a merged JobsReply would copy payloads)
+                jobs = list(reply.jobs)
+                size = sum(len(j.File) for j in jobs)
                 while size < self.max_batch_bytes:
                     try:
-                        if len(merged.jobs) < self.min_batch_jobs:
-                            more = self.reply_q.get(timeout=self.linger_s)
-                        else:
-                            more = self.reply_q.get_nowait()
+                        more = self._take(self.linger_s if len(jobs) < self.min_batch_jobs else None)
                     except queue.Empty:
                         break
-                    merged.jobs.extend(more.jobs)
+                    jobs.extend(more.jobs)
                     size += sum(len(j.File) for j in more.jobs)
-                reply = merged
+                reply = _Merged(jobs)
             process_incoming_job(reply, self.complete_q, self.processor)
 
     # handlers.rs:14-32
@@ -148,12 +195,16 @@ class Worker:
                                   metadata=((P.MAX_RECEIVE_KEY, str(self.max_receive)),))
         except grpc.RpcError:
             return  # empty queue / server gone: the reference ignores it (handlers.rs:59)
-        self.reply_q.put(reply)
+        self._put(reply)
 
     def run(self, duration: Optional[float] = None):
         CONNECTED.set()
         th = threading.Thread(target=self._compute, daemon=True, name="compute")
         th.start()
+        fetch = [threading.Thread(target=self._fetch, args=(i,), daemon=True, name=f"fetch{i}")
+                 for i in range(1, self.fetchers)]
+        for f in fetch:
+            f.start()
         t_end = None if duration is None else time.monotonic() + duration
         next_job = next_status = time.monotonic()
         try:
@@ -173,6 +224,8 @@ class Worker:
         finally:
             self.stop.set()
             th.join(timeout=5)
+            for f in fetch:
+                f.join(timeout=5)
             self.channel.close()
 
 
@@ -188,6 +241,8 @@ def main(argv=None):
                     help="merge queued JobsReplies into one GPU batch up to this size")
     ap.add_argument("--min-batch-jobs", type=int, default=0,
                     help="linger for more replies while a batch has fewer jobs")
+    ap.add_argument("--fetchers", type=int, default=1,
+                    help="RequestJobs connections kept busy (1: the reference's job tick only)")
     ap.add_argument("--duration", type=float, default=None)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
@@ -195,7 +250,7 @@ def main(argv=None):
     eng = Engine(grid, device=a.device)
     Worker(a.target, engine_processor(eng), a.cores,
            max_receive=a.max_receive_mb << 20, max_batch_bytes=a.max_batch_mb << 20,
-           min_batch_jobs=a.min_batch_jobs).run(a.duration)
+           min_batch_jobs=a.min_batch_jobs, fetchers=a.fetchers).run(a.duration)
 
 
 if __name__ == "__main__":

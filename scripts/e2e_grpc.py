@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16, help="jobs per RequestJobs (cores)")
     ap.add_argument("--max-batch-mb", type=int, default=0, help="worker-side reply merging")
     ap.add_argument("--min-batch-jobs", type=int, default=0, help="worker-side linger target")
+    ap.add_argument("--fetchers", type=int, default=1, help="worker RequestJobs connections")
     a = ap.parse_args()
     grid = D.config5_grid()
     tmp = tempfile.mkdtemp(prefix="dbx_e2e_")
@@ -44,7 +45,8 @@ def main():
     with D.Engine(grid, timing=True) as eng:
         w = WK.Worker(f"127.0.0.1:{port}", WK.engine_processor(eng), cores=a.batch,
                       job_tick=0.01, status_tick=0.5, max_receive=1 << 30,
-                      max_batch_bytes=a.max_batch_mb << 20, min_batch_jobs=a.min_batch_jobs)
+                      max_batch_bytes=a.max_batch_mb << 20, min_batch_jobs=a.min_batch_jobs,
+                      fetchers=a.fetchers)
         th = threading.Thread(target=w.run, daemon=True)
         t0 = time.perf_counter()
         th.start()
@@ -66,7 +68,7 @@ def main():
     evals = a.symbols * a.bars * grid.n_params
     n_lines = sum(len(v.strip().split("\n")) for v in disp.results.values())
     print(json.dumps({"workload": "config-5 pipeline, gRPC-fed, 1 GPU", "symbols": a.symbols,
-                      "bars": a.bars, "params": grid.n_params, "batch": a.batch, "max_batch_mb": a.max_batch_mb, "min_batch_jobs": a.min_batch_jobs,
+                      "bars": a.bars, "params": grid.n_params, "batch": a.batch, "max_batch_mb": a.max_batch_mb, "min_batch_jobs": a.min_batch_jobs, "fetchers": a.fetchers,
                       "payload_mb": sum(os.path.getsize(p) for p in paths) / 2**20,
                       "gen_s": t_gen, "wall_s": wall, "bar_evals_per_s_end_to_end": evals / wall,
                       "kernel": kname, "kernel_ms_total": kms, "launches": nl,

@@ -58,7 +58,7 @@ def oracle_processor(grid):
     return run
 
 
-def _run_e2e(tmp_path, processor, grid, cores=4, timeout=60):
+def _run_e2e(tmp_path, processor, grid, cores=4, timeout=60, **worker_kw):
     paths, closes = _write_files(tmp_path)
     disp = DSP.Dispatcher(paths)
     replies = []
@@ -71,7 +71,8 @@ def _run_e2e(tmp_path, processor, grid, cores=4, timeout=60):
         return rep
     disp.request_jobs = spy
     server, port = DSP.serve(disp, "127.0.0.1:0")
-    w = WK.Worker(f"127.0.0.1:{port}", processor, cores=cores, job_tick=0.05, status_tick=0.2)
+    w = WK.Worker(f"127.0.0.1:{port}", processor, cores=cores, job_tick=0.05, status_tick=0.2,
+                  **worker_kw)
     th = threading.Thread(target=w.run, daemon=True)
     t0 = time.time()
     th.start()
@@ -112,6 +113,18 @@ def test_config1_end_to_end_cpu_processor(tmp_path):
     _check_results(disp, paths, closes, grid)
 
 
+def test_extra_fetchers_complete_every_job_once(tmp_path):
+    """Worker with three RequestJobs connections (fetchers) and reply merging: every file is
+    handed out once (no re-dispatch), completed, and its results are the oracle's."""
+    grid = D.config2_grid()
+    disp, replies, paths, closes, wall = _run_e2e(tmp_path, oracle_processor(grid), grid, cores=2,
+                                                  fetchers=3, max_batch_bytes=1 << 20)
+    assert sorted(disp.job_paths.values()) == sorted(paths)  # each path handed out once
+    assert disp.requeued == 0
+    assert len({ctx for ctx in disp.peers}) >= 2  # the fetchers' own connections
+    _check_results(disp, paths, closes, grid)
+
+
 @pytest.mark.gpu
 def test_config1_end_to_end_gpu_engine(tmp_path):
     grid = D.config2_grid()
@@ -139,6 +152,24 @@ def test_wire_bytes_match_reference_contract(golden_dir):
     # field numbers/types of the other messages (proto:29-32)
     cr = P.CompleteRequest(id="i", data="d").SerializeToString()
     assert cr == b"\x0a\x01i\x12\x01d"
+    # the dispatcher's direct encoder writes the same bytes as the message runtime
+    assert P.encode_jobs_reply([("abc", b"t,o,h,l,c,v\n")]).hex() == pins["JobsReply{[Job{id:'abc', File:'t,o,h,l,c,v\\n'}]}"]
+
+
+def test_jobs_reply_encoder_matches_message_runtime():
+    """proto.encode_jobs_reply == JobsReply(...).SerializeToString(): empty ids / files (omitted
+    in proto3), multi-byte varints (127/128/16383/16384-byte and 2 MB payloads), many jobs, and
+    the dispatcher's Reply parses back to the same jobs."""
+    import random
+    rng = random.Random(7)
+    sizes = [0, 1, 127, 128, 16383, 16384, 2 << 20] + [rng.randrange(0, 5000) for _ in range(20)]
+    jobs = [(("" if i % 5 == 0 else str(rng.getrandbits(128))), bytes(rng.getrandbits(8) for _ in range(min(n, 64))) * (n // 64) + b"z" * (n % 64))
+            for i, n in enumerate(sizes)]
+    ref = P.JobsReply(jobs=[P.Job(id=j, File=f) for j, f in jobs]).SerializeToString()
+    assert P.encode_jobs_reply(jobs) == ref
+    assert P.encode_jobs_reply([]) == P.JobsReply().SerializeToString() == b""
+    back = P.JobsReply.FromString(DSP.Reply([DSP.Job(j, f) for j, f in jobs]).SerializeToString())
+    assert [(j.id, j.File) for j in back.jobs] == jobs
 
 
 def test_process_incoming_job_flag_and_order():
