@@ -576,9 +576,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int pj = ((iw * nk + ik) * g.nc + isl) * g.nd + itp;
     const int w = g.a[iw];
     const int32_t sl_bps = g.c[isl], tp_bps = g.d[itp];
-    // level factors (10000 -+ bps) * 1e-4 per side of the trade (level_y)
-    const double gl_long = (double)(10000 - sl_bps) * 1e-4, gl_short = (double)(10000 - tp_bps) * 1e-4;
-    const double gh_long = (double)(10000 + tp_bps) * 1e-4, gh_short = (double)(10000 + sl_bps) * 1e-4;
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
@@ -614,7 +611,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         r2[(T_scan * kTile) % R] = 0;
         // the distinct SL/TP distances (a level 1e4 -+ bps is shared by every SL and TP of that
         // bps: config 4's {50, 100} and {50, 100, 200, 400} make 4 levels per side, not 6) and
-        // their factors, the same as the walk's (gl_*, gh_*)
+        // their factors (level_y)
         int nu = 0;
         for (int o = 0; o < nlev; ++o) {
             const int32_t v = o < nsl ? g.c[o] : g.d[o - nsl];
@@ -827,8 +824,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // no high can exceed it then)
     auto set_levels = [&](int32_t cx, int np) {
         const double cd = (double)cx;
-        const double yl = level_y(cd, np > 0 ? gl_long : gl_short);
-        const double yh = level_y(cd, np > 0 ? gh_long : gh_short);
+        // level factors (10000 -+ bps) * 1e-4 of the trade's sides (level_y)
+        const double yl = level_y(cd, levf[np > 0 ? usl : utp]);
+        const double yh = level_y(cd, levf[nlev + (np > 0 ? utp : usl)]);
         XL = (int32_t)yl;
         XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
     };
@@ -903,7 +901,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     a.ps2 -= q2x;
                     acct_open(a, t0 + b, b, cx);
                     a.pos = np;
-                    set_levels(cx, np);
                     cur = b + 1;
                 }
                 if (cur >= kTile) return false;
@@ -923,7 +920,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 // signal exit that is the last close again, which leaves the aggregate unchanged)
                 if (hit) x = xs;
                 const int qi = hit ? x - 1 : x;  // >= a.sb - 1 (exits come after the entry bar)
-                const int32_t px = hit ? ((xlo < xhi || (xlo == xhi && lg)) ? XL : XHm1 + 1) : cT[x];
+                // fill price: the touched level (XHm1 + 1 = the upper level below 2^31); a trade
+                // entered in the tile computes only the level it hit (levels of a position still
+                // open at the tile end are set after the walk)
+                const bool low = xlo < xhi || (xlo == xhi && lg);
+                int32_t px = cT[min(x, kTile - 1)];
+                if (hit) {
+                    const int ul = lg ? usl : utp, uh = lg ? utp : usl;  // the trade's level rows
+                    const int32_t pe = (int32_t)level_y((double)a.ce, levf[low ? ul : nlev + uh]);
+                    px = (FIRST && !entered) ? (low ? XL : XHm1 + 1) : pe;
+                }
                 // qi < a.sb only for a fill at the first bar of the tile of a carried position;
                 // a trade opened in this tile exits after its entry bar a.sb, so qi >= a.sb
                 const Agg seg = dst_query_w(D, a.sb, FIRST ? max(qi, a.sb) : qi);
@@ -942,6 +948,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 while (trade(std::false_type{})) {
                 }
             }
+            if (a.pos != 0 && a.e >= t0) set_levels(a.ce, a.pos);  // entered here, still open
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
