@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void topk_collect(const uint64_t* __restrict__
     }
 }
 
-__global__ __launch_bounds__(1024) void topk_finish(
+__global__ __launch_bounds__(256) void topk_finish(
     const uint64_t* __restrict__ key, const bt_summary* __restrict__ sum,
     const SymDesc* __restrict__ syms, int32_t P, const unsigned int* __restrict__ counts,
     const unsigned long long* __restrict__ above, const unsigned long long* __restrict__ cand,
@@ -123,7 +123,10 @@ __global__ __launch_bounds__(1024) void topk_finish(
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         if (i < n) {
             const unsigned long long idx = i < n_above ? above[i] : cand[i - n_above];
-            const int s = (int)(idx / (unsigned long long)P), p = (int)(idx % (unsigned long long)P);
+            // 32-bit division whenever the index fits (a 64-bit one is a long software sequence)
+            const bool small = idx < (1ULL << 32);
+            const int s = small ? (int)((uint32_t)idx / (uint32_t)P) : (int)(idx / (unsigned long long)P);
+            const int p = (int)(idx - (unsigned long long)s * (unsigned long long)P);
             kk[i] = key[idx];
             ss[i] = ((uint64_t)(uint32_t)syms[s].id << 32) | (uint32_t)p;
             ix[i] = idx;
@@ -191,8 +194,11 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
                        int32_t P, int32_t k, const TopkWork& w, hipStream_t st) {
     if (n <= 0 || k <= 0) return hipSuccess;
     const unsigned long long need = (unsigned long long)(k < n ? k : n);
-    int64_t blocks = (n + 2047) / 2048;
-    if (blocks > 1024) blocks = 1024;
+    // few blocks, many keys per thread: each block adds its LDS histogram's non-empty bins to the
+    // global one with device-scope atomics that pile up on the few bins a Sharpe distribution
+    // fills (1,024 blocks made the chain ~0.34 ms per config-2 step, overlapped with the next kernel)
+    int64_t blocks = (n + 8191) / 8192;
+    if (blocks > 256) blocks = 256;
     for (int shift = 52; shift >= 40; shift -= 12) {
         hipLaunchKernelGGL(topk_hist, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
                            (const unsigned long long*)w.state, w.hist);
@@ -201,7 +207,9 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
     }
     hipLaunchKernelGGL(topk_collect, dim3((unsigned)blocks), dim3(256), 0, st, key, n,
                        (const unsigned long long*)w.state, w.counts, w.above, w.cand, w.cap);
-    hipLaunchKernelGGL(topk_finish, dim3(1), dim3(1024), (size_t)w.cap * 24, st, key, sum, syms,
+    // one small block (256 threads, the sort's 2,048 slots in 48 KB of LDS): it finds room on a CU
+    // beside the next step's strategy kernel sooner than a 1,024-thread block
+    hipLaunchKernelGGL(topk_finish, dim3(1), dim3(256), (size_t)w.cap * 24, st, key, sum, syms,
                        P, w.counts, w.above, w.cand, w.cap, k, w.out, w.out_n);
     hipLaunchKernelGGL(topk_reset, dim3(1), dim3(64), 0, st, w.state, w.counts);
     return hipGetLastError();
