@@ -394,6 +394,30 @@ def test_boll_many_k_values():
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
+@pytest.mark.parametrize("sl,tp", [
+    ([25, 50, 75, 100, 150], [50, 100, 200, 300, 400, 75]),   # 3 shared: 8 distinct levels
+    ([30, 9999, 120], [45, 9999]),                            # 4 distinct (odd pairs), extreme bps
+    ([60], [60]),                                             # one level for all four sides
+])
+def test_boll_sltp_level_sharing(sl, tp):
+    """SL/TP level tables built per *distinct* bps (a level 1e4 -+ bps serves every SL and TP of
+    that bps) and searched two per level task: grids with shared, odd-count and extreme
+    (9,999 bps) distances, bit-exact trades vs the oracle."""
+    grid = D.Grid.boll([10, 45], [3, 5], sl, tp, k_den=2)
+    bars = 3000
+    o, h, lo, c = _gen(0x5EED, [31, 32], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 31, 2, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(2):
+        orc, otr = oracle_row("boll", grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"boll levels sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
 def test_run_batch_binary_and_csv_mixed():
     """bt_run_batch on one JobsReply mixing DBXCOL1 payloads (decoded straight into the pinned
     staging rows), CSV text, and malformed payloads of every kind: good jobs bit-exact vs the
