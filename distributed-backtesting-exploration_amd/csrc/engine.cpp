@@ -207,6 +207,11 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             const int64_t kmax = std::max<int64_t>(c.k_den, *std::max_element(e->ax[1].begin(), e->ax[1].end()));
             if ((int64_t)e->grid.wmax * kmax >= (1LL << 32)) return "Bollinger grid outside the exact int128 range (window * k >= 2^32)";
             e->grid.ring = (e->grid.wmax + 4 * kTile - 1) / kTile * kTile;
+            for (int q = 0; q < 8; ++q) {
+                const int64_t kn = q < c.n_k ? e->ax[1][q] : 0;
+                e->grid.kn2[q] = (double)(kn * kn);  // exact: kn <= 2^20
+            }
+            e->grid.kmin_idx = (int32_t)(std::min_element(e->ax[1].begin(), e->ax[1].end()) - e->ax[1].begin());
             if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;
         }
@@ -332,8 +337,8 @@ void run_impl(bt_engine* e) {
     HIPCHK(hipMemsetAsync(e->d_ntr[b].p, 0, sizeof(unsigned long long), e->stream));
     out.dbg = nullptr;
     if (BT_ABL(e->grid, 64)) {  // profiling stamps (profiling build only)
-        e->d_dbg.ensure(32);
-        HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, 32 * sizeof(unsigned long long), e->stream));
+        e->d_dbg.ensure(64);
+        HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, 64 * sizeof(unsigned long long), e->stream));
         out.dbg = e->d_dbg.p;
     }
     const bool timing = (e->cfg.flags & BT_FLAG_TIMING) != 0;
@@ -1066,7 +1071,7 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n) 
 
 int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n) {
     ABI_GUARD(-1, {
-        if (!e || !out || n < 0 || n > 32 || !e->d_dbg.p) throw HipFail{"no debug stamps"};
+        if (!e || !out || n < 0 || n > 64 || !e->d_dbg.p) throw HipFail{"no debug stamps"};
         activate(e);
         sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_dbg.p, (size_t)n * 8, hipMemcpyDeviceToHost));

@@ -38,7 +38,10 @@ struct Grid {
     int32_t ring;                  // prefix ring length >= wmax + 3 kTile (SMA: a power of two;
                                    // tile kernels: a multiple of kTile)
     double sqrt_ann;               // sqrt((double)annualization), computed on the host
-    int32_t ablate;                // BT_PROFILING builds only (env BT_ABLATE): phases to skip;
+    double kn2[8];                 // Bollinger: k_num^2 of the first 8 k values (kernel arguments,
+                                   // so the z tests read them from scalar registers)
+    int32_t kmin_idx;              // Bollinger: index of the smallest k_num (the busiest lanes)
+    int32_t ablate;               // BT_PROFILING builds only (env BT_ABLATE): phases to skip;
                                    // always 0 in the release library (read through BT_ABL)
     const int32_t* a;              // device arrays
     const int32_t* b;

@@ -34,6 +34,12 @@ namespace bt {
 namespace {
 
 constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflict-free columns
+// Bollinger tile buffers: scanned (k+2), flagged (k+1), walked (k) and accounted (k-1, by the
+// accountant wave of a split walk)
+constexpr int kBollStages = 4;
+// Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
+// after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
+constexpr int kRecCap = 33;
 // Bollinger per-stage low/high staging (int32): lows[64], highs[64], 8 block minima of the lows
 // then 8 block maxima of the highs, per bar the minimum low / maximum high from that bar to the
 // end of its 8-bar block, and per bar the minimum low / maximum high from that bar to the end of
@@ -42,7 +48,7 @@ constexpr int kLH = 6 * kTile + 16;
 constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16, kLhTs = 4 * kTile + 16;
 
 struct TileLds {
-    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levf, lvb, ctr, total;
+    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levp, levf, lvb, rec, nrec, ctr, total;
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
@@ -51,19 +57,23 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
     TileLds L{};
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
+    const int ns = kind == 1 ? kBollStages : kTileStages;
     L.r1 = take((size_t)ring * 8);
     L.r2 = take((size_t)ring * (kind == 0 ? 8 : 16));
-    L.ct = take((size_t)kTileStages * kTile * 4);
-    L.ql = take((size_t)kTileStages * 2 * kTile * 8);
-    L.dst = take((size_t)kTileStages * kDstLevels * kTile * sizeof(Agg));
+    L.ct = take((size_t)ns * kTile * 4);
+    L.ql = take((size_t)ns * 2 * kTile * 8);
+    L.dst = take((size_t)ns * kDstLevels * kTile * sizeof(Agg));
     if (kind == 1) {
-        L.stl = take((size_t)kTileStages * kLH * 4);  // lows, highs, block and in-block suffix extrema
+        L.stl = take((size_t)ns * kLH * 4);  // lows, highs, block and in-block suffix extrema
         L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
         L.words = take((size_t)2 * (2 * na * nb + 2 * na) * 8);
         L.win = take((size_t)na * 4);
         L.lev = take((size_t)2 * 2 * nlev * kTile);  // first-passage bars, [tile & 1][side][level][bar]
+        L.levp = take((size_t)3 * 2 * nlev * kTile * 4);  // the levels (int32), [tile % 3][side][level][bar]
         L.levf = take((size_t)2 * nlev * 8);         // level factors per side
         L.lvb = take((size_t)(nlev + 1) * 4);        // distinct SL/TP bps, then their count
+        L.rec = take((size_t)2 * kRecCap * kTile * 2);  // trade records [tile & 1][record][lane]
+        L.nrec = take((size_t)2 * kTile);                // records per lane [tile & 1][lane]
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
@@ -99,6 +109,60 @@ __device__ __forceinline__ int ring_pos(int T, int lane, int R) {
 __device__ __forceinline__ int ring_back(int p, int W, int R) {
     const int q = p - W;
     return q < 0 ? q + R : q;
+}
+
+// x^2 for x < 2^64, unsigned 128-bit, from three 32 x 32 -> 64 products (the generic
+// 64 x 64 -> 128 multiply takes four and sign terms): x^2 = l^2 + 2 h l 2^32 + h^2 2^64.
+__device__ __forceinline__ unsigned __int128 sq_u64(uint64_t x) {
+    const uint32_t l = (uint32_t)x, h = (uint32_t)(x >> 32);
+    const uint64_t ll = (uint64_t)l * l, hl = (uint64_t)h * l, hh = (uint64_t)h * h;
+    const uint64_t mid_lo = hl << 33, mid_hi = hl >> 31;  // 2 h l 2^32 = mid_hi 2^64 + mid_lo
+    const uint64_t lo = ll + mid_lo;
+    const uint64_t hi = hh + mid_hi + (lo < ll ? 1 : 0);
+    return ((unsigned __int128)hi << 64) | lo;
+}
+
+// a * w for a < 2^96 and a 32-bit w (sums of squared prices: < 2^75), exact below 2^128.
+__device__ __forceinline__ unsigned __int128 mul_u128_u32(unsigned __int128 a, uint32_t w) {
+    const uint64_t lo = (uint64_t)a;
+    const uint32_t hi = (uint32_t)(a >> 64);
+    const uint64_t p0 = (uint64_t)(uint32_t)lo * w, p1 = (lo >> 32) * (uint64_t)w;
+    const uint64_t r_lo = p0 + (p1 << 32);
+    const uint64_t r_hi = (uint64_t)hi * w + (p1 >> 32) + (r_lo < p0 ? 1 : 0);
+    return ((unsigned __int128)r_hi << 64) | r_lo;
+}
+
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled.
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+// Lane mask of a condition (the builtin on the bool itself: HIP's __ballot(int) materialises the
+// condition in a VGPR and compares it again).
+__device__ __forceinline__ uint64_t ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// A lane mask as an opaque 64-bit scalar: a mask reassigned in a branch then merges as a scalar
+// value instead of a per-lane boolean rebuilt in a VGPR.
+__device__ __forceinline__ uint64_t sgpr64(uint64_t x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
+// Lane mask of a > b (fp64) straight from the compare's scalar destination (inactive lanes 0).
+__device__ __forceinline__ uint64_t vcmp_gt_f64(double a, double b) {
+    uint64_t m;
+    asm volatile("v_cmp_gt_f64_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+
+// v_writelane: lane L of v takes the wave-uniform x.
+template <int L>
+__device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(L));
 }
 
 // Bits [cur, 63] of a tile word (none for cur >= 64).
@@ -534,7 +598,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          const int32_t* __restrict__ low,
                                                          const int32_t* __restrict__ close,
                                                          Grid g, Out out, int nextra, int lpw,
-                                                         SegArgs sg, int fix_seg) {
+                                                         SegArgs sg, int fix_seg, int split_grp,
+                                                         uint32_t wave_map) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
     const int nsl = g.nc, ntp = g.nd, nlev = nsl + ntp;
@@ -553,18 +618,39 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // (low side: 1e4 - sl for longs' SL, 1e4 - tp for shorts' TP) or whose high does (high side:
     // 1e4 + tp, 1e4 + sl), 64 if none; the walk of a trade entered in the tile reads it
     uint8_t* levt = reinterpret_cast<uint8_t*>(smem + LL.lev);
+    // ... and the level of each (side, level, entry bar): low side floor(c_b (1e4 - bps) / 1e4)
+    // (lows <= it touch), high side that level minus one (highs > it touch; INT32_MAX when the
+    // level reaches 2^31): a trade entered in the tile reads both with its entry close
+    int32_t* levp = reinterpret_cast<int32_t*>(smem + LL.levp);
     double* levf = reinterpret_cast<double*>(smem + LL.levf);
     int32_t* lvb = reinterpret_cast<int32_t*>(smem + LL.lvb);
+    // split walk: the finder records its lanes' trades per tile, the accountant folds them a
+    // tile later
+    uint16_t* recs = reinterpret_cast<uint16_t*>(smem + LL.rec);
+    uint8_t* nrec = reinterpret_cast<uint8_t*>(smem + LL.nrec);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // waves: [0, npw) parameters, npw the helper, then `nextra` task-only waves
-    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra;
+    // wave_map: role of hardware wave w < 8 (4 bits each; the roles below are logical wave
+    // indices), so the heavy roles land on different SIMDs next to light ones
+    const int tid = threadIdx.x, lane = tid & 63, hw_wave = tid >> 6;
+    const int wave = hw_wave < 8 ? (int)((wave_map >> (4 * hw_wave)) & 15u) : hw_wave;
+    // waves: [0, npw) parameter groups, npw the helper, npw + 1 the accountant of a split walk,
+    // then `nextra` task-only waves. Without a split every parameter wave walks and accounts its
+    // lanes' trades (walker); with one, parameter wave split_grp (the group of the busiest z
+    // threshold, whose per-lane trade chain sets the tile time) only finds its trades
+    // (finder) and the accountant wave keeps their accounts, one tile behind.
+    const bool split = split_grp >= 0;
+    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra - (split ? 1 : 0);
     const bool helper = wave == npw;
+    const bool accountant = split && wave == npw + 1;
+    const bool finder = split && wave == split_grp;
+    const int grp = accountant ? split_grp : wave;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
-    const int j = (blockIdx.y * npw + wave) * lpw + lane;
-    const bool active = wave < npw && lane < lpw && j < P;
+    const int j = (blockIdx.y * npw + grp) * lpw + lane;
+    const bool active = (wave < npw || accountant) && lane < lpw && j < P;
+    const bool keeps = active && !finder;       // keeps accounts (walker or accountant)
+    const bool walks = active && !accountant;   // walks the condition words (walker or finder)
     // lanes run k-major (lane j -> (ik, iw, isl, itp)) while results keep the param order
     // ((iw * nk + ik) * nsl + isl) * ntp + itp: a wave then holds one z threshold, and the
     // threshold sets most of a lane's trade rate, so the walk (a wave iterates the maximum
@@ -594,7 +680,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         mine = sg.rec + sr.seg * per_seg + (size_t)blockIdx.x * P + pj;
         if (sr.seg > 0) prev = mine - per_seg;
         if (fix_seg > 0) {  // re-walk only if some lane's speculative start is not the true one
-            if (!__syncthreads_or(active && seg_start_differs(mine, prev))) return;
+            if (!__syncthreads_or(keeps && seg_start_differs(mine, prev))) return;
             if (tid == 0) atomicAdd(sg.refixed, 1ULL);
         }
     }
@@ -644,7 +730,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     int32_t cpre = 0, hpre = 0, lpre = 0;
 
     auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
-        const int s = T % kTileStages, t0 = T * kTile;
+        const int s = T % kBollStages, t0 = T * kTile;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
         const int pt = ring_pos(T, lane, R);
@@ -722,7 +808,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // condition words of tile T, windows grabbed dynamically (round T), lane = bar
     auto flags = [&](int T) {
         if (no_tasks) return;
-        const int s = T % kTileStages, t = T * kTile + lane;
+        const int s = T % kBollStages, t = T * kTile + lane;
         const int64_t c = cts[s * kTile + lane];
         uint64_t* Wd = words + (T & 1) * nword;
         const int ptop = ring_pos(T, lane, R);
@@ -739,17 +825,22 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const int32_t* LH = lhs_ + s * kLH;
                 const double cd = (double)c;
                 uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
+                int32_t* ptab = levp + ((T % 3) * 2 + side) * nlev * kTile;
                 // kLevPass levels: independent searches, all stored after all
                 {
                     int x[kLevPass];
+                    int32_t X[kLevPass];
 #pragma unroll
                     for (int u = 0; u < kLevPass; ++u) {
                         const double y = level_y(cd, levf[side * nlev + min(i + u, nu - 1)]);
-                        x[u] = side == 0 ? first_low(LH, lane + 1, (int32_t)y)
-                                         : first_high(LH, lane + 1, y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
+                        X[u] = side == 0 ? (int32_t)y : (y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
+                        x[u] = side == 0 ? first_low(LH, lane + 1, X[u]) : first_high(LH, lane + 1, X[u]);
                     }
 #pragma unroll
-                    for (int u = 0; u < kLevPass; ++u) tab[min(i + u, nu - 1) * kTile + lane] = (uint8_t)x[u];
+                    for (int u = 0; u < kLevPass; ++u) {
+                        tab[min(i + u, nu - 1) * kTile + lane] = (uint8_t)x[u];
+                        ptab[min(i + u, nu - 1) * kTile + lane] = X[u];
+                    }
                 }
                 o = grab_value(vn) - base;
                 continue;
@@ -758,39 +849,57 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
             const int pj = ring_back(ptop, Wn, R);
-            const int64_t S1 = (int64_t)(P1t - r1[pj]);
+            // window sums: S1 = sum c in [0, 2^44) (prices < 2^31, windows < 2^13), S2 = sum c^2
+            const uint64_t S1 = P1t - r1[pj];
             const unsigned __int128 S2 = P2t - r2[pj];
-            const int64_t Dv = (int64_t)Wn * c - S1;
-            const i128 Q = (i128)Wn * (i128)S2 - (i128)S1 * (i128)S1;  // >= 0 on valid bars
-            // fp64 fast path: |z| > k <=> Dv^2 kd^2 > kn^2 Q, both sides within 2^-50 relative
+            const int64_t Dv = (int64_t)Wn * c - (int64_t)S1;
+            const unsigned __int128 Q = mul_u128_u32(S2, (uint32_t)Wn) - sq_u64(S1);  // >= 0 on valid bars
+            // fp64 fast path: |z| > k <=> Dv^2 kd^2 > kn^2 Q. |Dv| < 2^53 converts exactly; lh and
+            // rh = kn^2 Q (Q < 2^87: (Q >> 32) < 2^55 rounds once, the low word once more, the
+            // product once) are within 2^-50 relative of the exact sides. lhd = lh (1 - 2^-48) > rh
+            // then proves L > R and lhu = lh (1 + 2^-48) < rh proves L < R; a valid lane with
+            // neither (both sides zero included) is settled exactly in int128 with its whole wave.
             const double Dd = (double)Dv;
             const double lh = (Dd * Dd) * kd2d;
-            // Q < 2^87: (Q >> 32) < 2^55 rounds once, the low word adds one more rounding
-            const double Qd = (double)(int64_t)(Q >> 32) * 0x1p32 + (double)(uint32_t)Q;
-#pragma unroll 1
-            for (int q0 = 0; q0 < nk; q0 += kMaxK) {  // one pass for grids of <= 8 k values
-#pragma unroll
-            for (int qq = 0; qq < kMaxK; ++qq) {
-                const int q = q0 + qq;
-                if (q >= nk) break;
-                const double rh = kn2d[q] * Qd;
-                // lh and rh are within 2^-50 relative of the exact sides: outside a 2^-48 band
-                // the fp64 order is the exact order (both zero lands in the band)
-                bool big = lh > rh * (1.0 + 0x1p-48);
-                const bool amb = valid && !big && !(lh < rh * (1.0 - 0x1p-48));
-                if (__ballot(amb)) {  // rare: settle the whole wave exactly in int128
+            const double lhd = lh * (1.0 - 0x1p-48), lhu = lh * (1.0 + 0x1p-48);
+            const double Qd = (double)(uint64_t)(Q >> 32) * 0x1p32 + (double)(uint32_t)Q;
+            const uint64_t vm = ballot(valid);
+            const uint64_t dp = ballot(valid && Dv >= 0), dn = ballot(valid && Dv <= 0);
+            const uint64_t zneg = vm & ~dp, zpos = vm & ~dn;  // Dv < 0, Dv > 0
+            // the z words of one k: lane 0 .. 4 kMaxK - 1 of `zw` collect them (v_writelane, lane
+            // = dword of Wd[2 (ow nk + q) + side]), one store per pass of kMaxK values
+            auto ztest = [&](auto qtag, int q, double kn2, uint32_t& zw) {
+                constexpr int qq = decltype(qtag)::value;
+                const double rh = kn2 * Qd;
+                uint64_t big = vcmp_gt_f64(lhd, rh) & vm;
+                const uint64_t small = vcmp_gt_f64(rh, lhu);
+                if (vm & ~big & ~small) {  // rare: settle the whole wave exactly in int128
                     const int64_t kn = g.b[q];
-                    big = (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * Q;
+                    big = sgpr64(ballot(valid && (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * (i128)Q));
                 }
-                const uint64_t zl = __ballot(valid && big && Dv < 0);
-                const uint64_t zh = __ballot(valid && big && Dv > 0);
-                if (lane == 0) {
-                    Wd[2 * (ow * nk + q)] = zl;
-                    Wd[2 * (ow * nk + q) + 1] = zh;
-                }
+                const uint64_t zl = big & zneg, zh = big & zpos;
+                writelane<4 * qq>(zw, (uint32_t)zl);
+                writelane<4 * qq + 1>(zw, (uint32_t)(zl >> 32));
+                writelane<4 * qq + 2>(zw, (uint32_t)zh);
+                writelane<4 * qq + 3>(zw, (uint32_t)(zh >> 32));
+            };
+            {  // first pass: k_num^2 from the kernel arguments
+                uint32_t zw = 0;
+                static_for<kMaxK>([&](auto qtag) {
+                    constexpr int qq = decltype(qtag)::value;
+                    if (qq < nk) ztest(qtag, qq, g.kn2[qq], zw);
+                });
+                if (lane < 4 * min(nk, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * ow * nk)[lane] = zw;
             }
+#pragma unroll 1
+            for (int q0 = kMaxK; q0 < nk; q0 += kMaxK) {  // grids of more than 8 k values
+                uint32_t zw = 0;
+                static_for<kMaxK>([&](auto qtag) {
+                    constexpr int qq = decltype(qtag)::value;
+                    if (q0 + qq < nk) ztest(qtag, q0 + qq, kn2d[q0 + qq], zw);
+                });
+                if (lane < 4 * min(nk - q0, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * (ow * nk + q0))[lane] = zw;
             }
-            const uint64_t dp = __ballot(valid && Dv >= 0), dn = __ballot(valid && Dv <= 0);
             if (lane == 0) {
                 Wd[2 * nw * nk + 2 * ow] = dp;
                 Wd[2 * nw * nk + 2 * ow + 1] = dn;
@@ -818,8 +927,10 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     TradeAcct a;
     acct_init(a);
-    // open trade: lows <= XL hit the low-side level, highs > XHm1 the high-side level
+    // open trade: lows <= XL hit the low-side level, highs > XHm1 the high-side level (the
+    // walker's and finder's copy; the accountant keeps its own for the fill prices)
     int32_t XL = 0, XHm1 = 0;
+    int fpos = 0;  // finder: position carried between tiles (its only state besides the levels)
     // low-side level: long SL / short TP (< ce); high-side: long TP / short SL (may reach 2^31:
     // no high can exceed it then)
     auto set_levels = [&](int32_t cx, int np) {
@@ -834,16 +945,32 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     if (SEG && fix_seg > 0 && active) {  // the true state entering the segment
         seg_inject(a, prev);
         if (a.pos != 0) set_levels(a.ce, a.pos);
+        fpos = a.pos;
         start_pos = a.pos;
         start_e = a.e;
     }
     const size_t gi = (size_t)blockIdx.x * P + pj;
-    bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
+    bt_trade* tr = (PARITY && keeps) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
+
+    // Close the open trade at in-tile bar x (exit kind: SL/TP fill at px, else the close at x),
+    // given D / ql of its tile and the trade's sparse-table query index qi (the bar before a
+    // fill, the exit bar of a signal exit): the path is the carried aggregate (kAggId for a
+    // trade opened in this tile), the tile's closes [a.sb, qi] and the fill price.
+    auto close_trade = [&](int t0, int x, int qi, int32_t px, const Agg& seg, int64_t qx, int64_t q2x) {
+        const bool lg = a.pos > 0;
+        const Agg sp = qi < a.sb ? kAggId : seg;
+        const Agg st = agg_merge(agg_merge(a.agg, sp), agg_one(px));
+        acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
+        a.ps1 += lg ? (uint64_t)qx : (uint64_t)0 - (uint64_t)qx;
+        a.ps2 += (uint64_t)q2x;
+        a.pos = 0;
+    };
 
     StampAcc sa;
     if (STAMPS) sa.begin();
-    for (int k = T_scan; k < T_end; ++k) {
+    // a split walk's accountant folds tile k - 1 in step k: one step more
+    for (int k = T_scan; k < T_end + (split ? 1 : 0); ++k) {
         const int t0 = k * kTile;
         if (helper && k + 2 < T_end) {
             scan(k + 2, cpre, hpre, lpre);
@@ -853,16 +980,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             lpre = ldc(lrow, B, tn, INT32_MAX);
         }
         if (STAMPS) sa.mark(0);
-        if (SEG && k == T_acct && active) {
+        // the tile whose accounts this lane advances in this step
+        const int ka = accountant ? k - 1 : k;
+        if (SEG && ka == T_acct && keeps) {
             // first accounted tile: keep the state the (speculative) walk reached, drop the
             // burn-in's sums (a trade open here is closed and accounted in this segment)
             start_pos = a.pos;
             start_e = a.e;
             seg_reset_sums(a);
         }
-        if (active && k >= T_walk && !BT_ABL(g, 8)) {
+        if (walks && k >= T_walk && k < T_end && !BT_ABL(g, 8)) {
             __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
-            const int s = k % kTileStages;
+            const int s = k % kBollStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
             const Agg* D = dst + s * kDstLevels * kTile;
@@ -877,78 +1006,199 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const uint64_t DN = (W[2 * nw * nk + 2 * iw + 1] & vm) | fb;
             const uint8_t* TL = levt + (k & 1) * 2 * nlev * kTile;  // first-passage tables
             const uint8_t* TH = TL + nlev * kTile;
-            int cur = 0;
-            // one trade (entry and/or exit) per call, in bar order; false when the tile is done.
-            // Only the first trade of the tile can start open (path carried in a.agg)
-            auto trade = [&](auto first_tag) -> bool {
-                constexpr bool FIRST = decltype(first_tag)::value;
-                if (STAMPS) sa.count(3);
-                int xlo = kTile, xhi = kTile;
-                bool entered = false;
-                if (!FIRST || a.pos == 0) {
-                    const uint64_t m = (ZL | ZH) & bits_from(cur);
-                    if (m == 0) return false;
-                    const int b = __builtin_ctzll(m);
-                    const int np = ((ZL >> b) & 1) ? 1 : -1;
-                    const int32_t cx = cT[b];
-                    const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
-                    // this trade's SL/TP first passages in the tile, read with the entry bar's
-                    // close and returns (one round trip)
-                    xlo = TL[(np > 0 ? lev_lo_long : lev_lo_short) * kTile + b];
-                    xhi = TH[(np > 0 ? lev_hi_long : lev_hi_short) * kTile + b];
-                    entered = true;
-                    a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
-                    a.ps2 -= q2x;
-                    acct_open(a, t0 + b, b, cx);
-                    a.pos = np;
-                    cur = b + 1;
-                }
-                if (cur >= kTile) return false;
-                // exit: first of SL/TP (intrabar, from entry + 1; SL wins a same-bar tie), the
-                // signal exit and the forced exit at B-1 (SL/TP beat both on the same bar)
-                const bool lg = a.pos > 0;
-                const uint64_t sig = (lg ? DP : DN) & (~0ULL << cur);  // cur < 64 here
-                int x = sig ? __builtin_ctzll(sig) : kTile;
-                // a position carried into the tile searches with its levels; a trade entered in
-                // it has its first passages from the tables
-                if (FIRST && !entered) sltp_search(LO, cur, XL, XHm1, xlo, xhi);
-                const int xs = min(xlo, xhi);
-                const bool hit = xs < kTile && xs <= x;
-                if (!hit && x >= kTile) return false;
-                // one path for both exit kinds (no divergence): the trade's closes up to the bar
-                // before an SL/TP fill or up to a signal exit's bar, then the fill price (for a
-                // signal exit that is the last close again, which leaves the aggregate unchanged)
-                if (hit) x = xs;
-                const int qi = hit ? x - 1 : x;  // >= a.sb - 1 (exits come after the entry bar)
-                // fill price: the touched level (XHm1 + 1 = the upper level below 2^31); a trade
-                // entered in the tile computes only the level it hit (levels of a position still
-                // open at the tile end are set after the walk)
-                const bool low = xlo < xhi || (xlo == xhi && lg);
-                int32_t px = cT[min(x, kTile - 1)];
-                if (hit) {
-                    const int ul = lg ? usl : utp, uh = lg ? utp : usl;  // the trade's level rows
-                    const int32_t pe = (int32_t)level_y((double)a.ce, levf[low ? ul : nlev + uh]);
-                    px = (FIRST && !entered) ? (low ? XL : XHm1 + 1) : pe;
-                }
-                // qi < a.sb only for a fill at the first bar of the tile of a carried position;
-                // a trade opened in this tile exits after its entry bar a.sb, so qi >= a.sb
-                const Agg seg = dst_query_w(D, a.sb, FIRST ? max(qi, a.sb) : qi);
-                const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
-                const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
-                const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
-                a.ps1 += lg ? qx : (uint64_t)0 - qx;
-                a.ps2 += q2x;
-                a.pos = 0;
-                cur = x + 1;
-                return true;
-            };
-            if (trade(std::true_type{})) {
+            const int32_t* PL = levp + (k % 3) * 2 * nlev * kTile;  // levels
+            const int32_t* PH = PL + nlev * kTile;
+            if (!finder) {
+                int cur = 0;
+                // walker: one trade (entry and/or exit) per call, in bar order; false when the
+                // tile is done. Only the first trade of the tile can start open (path carried in
+                // a.agg). Two LDS round trips per trade: everything the entry bar decides (close,
+                // returns, both sides' first passages and levels), then everything the exit bar
+                // decides (close, returns, the path's sparse-table entries), each issued together
+                // before any branch.
+                auto trade = [&](auto first_tag) -> bool {
+                    constexpr bool FIRST = decltype(first_tag)::value;
+                    if (STAMPS) sa.count(3);
+                    int xlo = kTile, xhi = kTile;
+                    bool entered = false;
+                    if (!FIRST || a.pos == 0) {
+                        const uint64_t m = (ZL | ZH) & bits_from(cur);
+                        if (m == 0) return false;
+                        const int b = __builtin_ctzll(m);
+                        const int np = ((ZL >> b) & 1) ? 1 : -1;
+                        const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
+                        const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
+                        const int32_t cx = cT[b];
+                        const int64_t qx = ql[b], q2x = ql[kTile + b];
+                        const int32_t pl = PL[rl], ph = PH[rh];
+                        xlo = TL[rl];
+                        xhi = TH[rh];
+                        asm volatile("" ::"v"(cx), "v"(qx), "v"(q2x), "v"(pl), "v"(ph), "v"(xlo), "v"(xhi));
+                        entered = true;
+                        a.ps1 += np > 0 ? (uint64_t)0 - (uint64_t)qx : (uint64_t)qx;
+                        a.ps2 -= (uint64_t)q2x;
+                        acct_open(a, t0 + b, b, cx);
+                        a.pos = np;
+                        XL = pl;
+                        XHm1 = ph;
+                        cur = b + 1;
+                    }
+                    if (cur >= kTile) return false;
+                    // exit: first of SL/TP (intrabar, from entry + 1; SL wins a same-bar tie),
+                    // the signal exit and the forced exit at B-1 (SL/TP beat both on the same bar)
+                    const bool lg = a.pos > 0;
+                    const uint64_t sig = (lg ? DP : DN) & (~0ULL << cur);  // cur < 64 here
+                    int x = sig ? __builtin_ctzll(sig) : kTile;
+                    // a position carried into the tile searches with its levels; a trade entered
+                    // in it has its first passages from the tables
+                    if (FIRST && !entered) sltp_search(LO, cur, XL, XHm1, xlo, xhi);
+                    const int xs = min(xlo, xhi);
+                    const bool hit = xs < kTile && xs <= x;
+                    if (hit) x = xs;
+                    // one path for both exit kinds (no divergence): the trade's closes up to the
+                    // bar before an SL/TP fill or up to a signal exit's bar, then the fill price
+                    // (for a signal exit that is the last close again, which leaves the aggregate
+                    // unchanged). With no exit in the tile (x = 64) the reads are clamped, issued
+                    // and unused.
+                    const int xc = min(x, kTile - 1);
+                    const int qi = hit ? x - 1 : xc;  // >= a.sb - 1 (exits follow the entry bar)
+                    // qi < a.sb only for a fill at the first bar of the tile of a carried
+                    // position; a trade opened in this tile exits after its entry bar a.sb
+                    const Agg seg = dst_query_w(D, a.sb, FIRST ? max(qi, a.sb) : qi);
+                    const int32_t cxx = cT[xc];
+                    const int64_t qx = ql[xc], q2x = ql[kTile + xc];
+                    asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
+                    if (!hit && x >= kTile) return false;
+                    // fill price: the touched level (XHm1 + 1 = the upper level below 2^31)
+                    const bool low = xlo < xhi || (xlo == xhi && lg);
+                    const int32_t px = hit ? (low ? XL : XHm1 + 1) : cxx;
+                    const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
+                    const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
+                    acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
+                    a.ps1 += lg ? (uint64_t)qx : (uint64_t)0 - (uint64_t)qx;
+                    a.ps2 += (uint64_t)q2x;
+                    a.pos = 0;
+                    cur = x + 1;
+                    return true;
+                };
+                if (trade(std::true_type{})) {
 #pragma unroll 1
-                while (trade(std::false_type{})) {
+                    while (trade(std::false_type{})) {
+                    }
+                }
+                if (STAMPS) sa.mark(1);
+                acct_tile_end(a, D, ql);
+            } else {
+                // finder: the same walk without the accounts; each trade leaves a 16-bit record
+                // [tile & 1][record][lane]: bits 0-5 entry bar, 6 entered in this tile, 7 long,
+                // 8-13 exit bar, 14-15 exit kind (0 still open, 1 signal / forced exit at the
+                // close, 2 low-level fill, 3 high-level fill)
+                uint16_t* RB = recs + (k & 1) * kRecCap * kTile + lane;
+                int nr = 0, fcur = 0;
+                bool first = true;  // wave-uniform: only the first trade can start open
+#pragma unroll 1
+                while (true) {
+                    if (STAMPS) sa.count(3);
+                    int xlo = kTile, xhi = kTile;
+                    bool entered = false;
+                    uint32_t rec;
+                    if (!first || fpos == 0) {
+                        const uint64_t m = (ZL | ZH) & bits_from(fcur);
+                        if (m == 0) break;
+                        const int b = __builtin_ctzll(m);
+                        const int np = ((ZL >> b) & 1) ? 1 : -1;
+                        const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
+                        const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
+                        const int32_t pl = PL[rl], ph = PH[rh];
+                        xlo = TL[rl];
+                        xhi = TH[rh];
+                        asm volatile("" ::"v"(pl), "v"(ph), "v"(xlo), "v"(xhi));
+                        entered = true;
+                        fpos = np;
+                        XL = pl;
+                        XHm1 = ph;
+                        fcur = b + 1;
+                        rec = (uint32_t)b | 64u | (np > 0 ? 128u : 0u);
+                    } else {
+                        rec = fpos > 0 ? 128u : 0u;
+                    }
+                    // one record store per trade; an entry at the tile's last bar or with no exit
+                    // in the tile leaves an open record, a carried position with no exit none
+                    bool emit = true, more = false;
+                    int x = kTile;
+                    if (fcur < kTile) {
+                        const bool lg = fpos > 0;
+                        const uint64_t sig = (lg ? DP : DN) & (~0ULL << fcur);
+                        x = sig ? __builtin_ctzll(sig) : kTile;
+                        if (first && !entered) sltp_search(LO, fcur, XL, XHm1, xlo, xhi);
+                        const int xs = min(xlo, xhi);
+                        const bool hit = xs < kTile && xs <= x;
+                        if (hit) x = xs;
+                        if (hit || x < kTile) {
+                            const bool low = xlo < xhi || (xlo == xhi && lg);
+                            rec |= ((uint32_t)x << 8) | ((hit ? (low ? 2u : 3u) : 1u) << 14);
+                            more = true;
+                        } else {
+                            emit = entered;
+                        }
+                    }
+                    if (emit) {
+                        RB[nr * kTile] = (uint16_t)rec;
+                        ++nr;
+                    }
+                    if (!more) break;
+                    fpos = 0;
+                    fcur = x + 1;
+                    first = false;
+                }
+                nrec[(k & 1) * kTile + lane] = (uint8_t)nr;
+                if (STAMPS) sa.mark(1);
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (accountant && active && ka >= T_walk && ka < T_end && !BT_ABL(g, 8)) {
+            // accountant: the finder's records of tile ka, in order (the tile's buffers stay
+            // until step ka + 2: four stages, levels in three)
+            __builtin_amdgcn_s_setprio(2);
+            const int s = ka % kBollStages, ta = ka * kTile;
+            const int32_t* cT = cts + s * kTile;
+            const int64_t* ql = qls + s * 2 * kTile;
+            const Agg* D = dst + s * kDstLevels * kTile;
+            const int32_t* PL = levp + (ka % 3) * 2 * nlev * kTile;
+            const int32_t* PH = PL + nlev * kTile;
+            const uint16_t* RB = recs + (ka & 1) * kRecCap * kTile + lane;
+            const int n = nrec[(ka & 1) * kTile + lane];
+#pragma unroll 1
+            for (int i = 0; i < n; ++i) {
+                if (STAMPS) sa.count(3);
+                const uint32_t rec = RB[i * kTile];
+                const int b = (int)(rec & 63u), x = (int)((rec >> 8) & 63u), kind = (int)(rec >> 14);
+                if (rec & 64u) {  // entry at b
+                    const int np = (rec & 128u) ? 1 : -1;
+                    const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
+                    const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
+                    const int32_t cx = cT[b];
+                    const int64_t qx = ql[b], q2x = ql[kTile + b];
+                    const int32_t pl = PL[rl], ph = PH[rh];
+                    asm volatile("" ::"v"(cx), "v"(qx), "v"(q2x), "v"(pl), "v"(ph));
+                    a.ps1 += np > 0 ? (uint64_t)0 - (uint64_t)qx : (uint64_t)qx;
+                    a.ps2 -= (uint64_t)q2x;
+                    acct_open(a, ta + b, b, cx);
+                    a.pos = np;
+                    XL = pl;
+                    XHm1 = ph;
+                }
+                if (kind != 0) {  // exit at x
+                    const bool hit = kind >= 2;
+                    const int qi = hit ? x - 1 : x;
+                    const Agg seg = dst_query_w(D, a.sb, max(qi, a.sb));
+                    const int32_t cxx = cT[x];
+                    const int64_t qx = ql[x], q2x = ql[kTile + x];
+                    asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
+                    const int32_t px = hit ? (kind == 2 ? XL : XHm1 + 1) : cxx;
+                    close_trade(ta, x, qi, px, seg, qx, q2x);
                 }
             }
-            if (a.pos != 0 && a.e >= t0) set_levels(a.ce, a.pos);  // entered here, still open
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
@@ -958,13 +1208,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         __syncthreads();
         if (STAMPS) sa.barrier();
     }
-    if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helper ? 1 : 3), lane);
+    // roles: parameter waves 0-3 by wave (k-major lanes: wave 0 holds the busiest threshold), 4 the
+    // helper, 5 the task-only waves, 6 the accountant
+    if (STAMPS) sa.flush(out.dbg, wave < npw ? min(wave, 3) : (helper ? 4 : (accountant ? 6 : 5)), lane);
+    // stamps: the raw HW_ID (SIMD in bits 4-5, CU in bits 8-11) of block 0's first 8 waves
+    if (STAMPS && blockIdx.x == 0 && blockIdx.z == 0 && lane == 0 && hw_wave < 8 && out.dbg != nullptr)
+        out.dbg[56 + hw_wave] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) + 1;
     if (SEG) {
-        if (active) seg_write(a, start_pos, start_e, mine);
+        if (keeps) seg_write(a, start_pos, start_e, mine);
         return;
     }
-    if (active) acct_write(a, B, g.sqrt_ann, gi, out);
-    wave_add_trades(out, active ? a.ntr : 0);
+    if (keeps) acct_write(a, B, g.sqrt_ann, gi, out);
+    wave_add_trades(out, keeps ? a.ntr : 0);
 }
 
 // Folds the bar segments of every (symbol, param) in order: additive counts, pnl, hash and
@@ -1023,6 +1278,39 @@ static int tile_param_waves(int need, int cap) {
     if (const char* v = getenv("BT_PW")) pw = std::max(1, std::min(atoi(v), pw));  // tuning aid
 #endif
     return pw;
+}
+
+// Hardware wave -> role of a Bollinger block (k_tile boll_tile_kernel wave_map). Hardware wave w
+// runs on SIMD w % 4, so waves w and w + 4 share one: each busy parameter wave (the walks, the
+// busiest first) gets a task-only wave as its partner (task waves take fewer tasks when their
+// SIMD is busy), the lightest parameter wave the helper, and the accountant of a split walk a
+// light parameter wave. Identity for blocks other than 8 waves.
+static uint32_t boll_wave_map(int pw, int split_grp, int xw) {
+    uint32_t m = 0;
+    for (int w = 0; w < 8; ++w) m |= (uint32_t)w << (4 * w);
+    const int nw = pw + 1 + (split_grp >= 0 ? 1 : 0) + xw;
+    if (nw == 8 && pw == 4) {
+        // logical roles: 0-3 parameter groups, 4 helper, then (split) 5 accountant, then tasks
+        const int split_map[8] = {0, 1, 2, 3, 6, 7, 5, 4};
+        const int plain_map[8] = {0, 1, 2, 3, 5, 6, 7, 4};
+        const int* r = split_grp >= 0 ? split_map : plain_map;
+        m = 0;
+        for (int w = 0; w < 8; ++w) m |= (uint32_t)r[w] << (4 * w);
+    }
+#ifdef BT_PROFILING
+    if (const char* v = getenv("BT_WAVEMAP")) m = (uint32_t)strtoul(v, nullptr, 16);  // tuning aid
+#endif
+    return m;
+}
+
+// Split Bollinger walk (finder + accountant waves) on by default; BT_SPLIT=0 turns it off in the
+// profiling build (A/B aid).
+static bool tile_split_walk() {
+    bool on = true;
+#ifdef BT_PROFILING
+    if (const char* v = getenv("BT_SPLIT")) on = atoi(v) != 0;
+#endif
+    return on;
 }
 
 static int tile_lanes_per_wave() {
@@ -1126,32 +1414,43 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 1);
     const bool split = seg.G > 1 && !parity;
     const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw), split ? seg.G : 1);
+    // Split walk: the parameter wave holding the smallest z threshold (lanes run k-major) trades
+    // the most, and its lanes' serial trade chains set the tile time (config 4: 7.1 walk
+    // iterations per tile against 1.0-4.3 for the other waves), so that wave only finds trades
+    // and an accountant wave keeps their accounts a tile later.
+    int split_grp = -1;
+    if (tile_split_walk() && pw >= 2 && grid.y == 1) {
+        const int grp = (int)(((long long)g.kmin_idx * g.na * g.nc * g.nd) / lpw);
+        if (grp < pw) split_grp = grp;
+    }
+    const int base = pw + 1 + (split_grp >= 0 ? 1 : 0);
     // at most one block per CU (config 4 on 8 GPUs: 250 symbols) leaves wave slots free: four
     // task-only waves (8.17 -> 7.90 ms vs two); otherwise as many as keep the block at 8 waves,
     // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms)
     const bool sparse = (long long)grid.x * grid.y * grid.z <= device_cus();
-    const int xw = tile_extra_waves(pw + 1, sparse ? 4 : std::max(2, std::min(3, 8 - (pw + 1))));
-    const dim3 block(64 * (pw + 1 + xw));
+    const int xw = tile_extra_waves(base, sparse ? 4 : std::max(2, std::min(3, 8 - base)));
+    const dim3 block(64 * (base + xw));
     const size_t lds = boll_lds_bytes(g);
+    const uint32_t wmap = boll_wave_map(pw, split_grp, xw);
 #ifdef BT_PROFILING
     if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
         return hipGetLastError();
     }
 #endif
     if (split) {
         // speculative segments, then the fix pass of each boundary in order (a block returns at
         // once when its lanes' starts were right), then the fold
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
         const dim3 fgrid(grid.x, grid.y, 1);
         for (int s = 1; s < seg.G; ++s)
-            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s);
+            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s, split_grp, wmap);
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
     } else if (parity) {
-        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
     } else {
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
     }
     return hipGetLastError();
 }
