@@ -666,6 +666,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
     const int nword = 2 * nw * nk + 2 * nw;
+    const int winreg = lane < nw ? g.a[lane] : 1;  // window lengths, lane = window (no LDS trip)
     const int64_t kd2 = (int64_t)g.k_den * g.k_den;
     const double kd2d = (double)kd2;
 
@@ -800,6 +801,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         LH[kLhTs + kTile + lane] = tmx;
     };
 
+    StampAcc sa;
     // with two or more task-only waves the parameter waves only walk (at raised priority)
     const bool walk_only = kWalkOnly && nextra >= 2;
     const bool no_tasks = walk_only && wave < npw;
@@ -820,6 +822,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         while (o < (uint32_t)ntask) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
             const int ow = (int)o, ol = ow - nw;  // window task ow, or level task ol
+            const uint64_t tt0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
             if (ol >= 0) {  // level task: lane = entry bar b, first passage from b + 1
                 const int side = ol & 1, i = ol >> 1 << kLevPassLog;
                 const int32_t* LH = lhs_ + s * kLH;
@@ -842,10 +845,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         ptab[min(i + u, nu - 1) * kTile + lane] = X[u];
                     }
                 }
+                if (STAMPS) sa.task[1] += __builtin_amdgcn_s_memtime() - tt0;
                 o = grab_value(vn) - base;
                 continue;
             }
-            const int Wn = win[ow];
+            const int Wn = nw <= 64 ? __builtin_amdgcn_readlane(winreg, ow & 63) : win[ow];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
             const int pj = ring_back(ptop, Wn, R);
@@ -904,6 +908,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 Wd[2 * nw * nk + 2 * ow] = dp;
                 Wd[2 * nw * nk + 2 * ow + 1] = dn;
             }
+            if (STAMPS) sa.task[0] += __builtin_amdgcn_s_memtime() - tt0;
             o = grab_value(vn) - base;
         }
     };
@@ -967,7 +972,6 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         a.pos = 0;
     };
 
-    StampAcc sa;
     if (STAMPS) sa.begin();
     // a split walk's accountant folds tile k - 1 in step k: one step more
     for (int k = T_scan; k < T_end + (split ? 1 : 0); ++k) {

@@ -245,9 +245,11 @@ __device__ __forceinline__ void seg_write(const TradeAcct& a, int start_pos, int
 
 // Diagnostic s_memtime stamps (Grid::ablate & 64 builds only): per role (0 = parameter waves,
 // 1 = helper A, 2 = helper B) the cycles spent working and waiting at the tile barrier.
-// dbg[8 * role + {0, 1, 2..5, 7}] = work, barrier, marked segments / counts, waves.
+// dbg[8 * role + {0, 1, 2..5, 6, 7}] = work, barrier, marked segments / counts, condition-word
+// task cycles, waves; dbg[64 + role] = level-task cycles.
 struct StampAcc {
     uint64_t prev = 0, w = 0, b = 0, x[4] = {0, 0, 0, 0};
+    uint64_t task[2] = {0, 0};  // cycles inside condition-word (0) and level (1) tasks
     __device__ __forceinline__ void begin() { prev = __builtin_amdgcn_s_memtime(); }
     __device__ __forceinline__ void mark(int i) {  // work segment i (counted into w as well)
         const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -272,6 +274,8 @@ struct StampAcc {
             atomicAdd(&dbg[8 * role + 1], (unsigned long long)b);
             for (int i = 0; i < 4; ++i) atomicAdd(&dbg[8 * role + 2 + i], (unsigned long long)x[i]);
             atomicAdd(&dbg[8 * role + 7], 1ULL);
+            atomicAdd(&dbg[8 * role + 6], (unsigned long long)task[0]);
+            atomicAdd(&dbg[64 + role], (unsigned long long)task[1]);
         }
     }
 };

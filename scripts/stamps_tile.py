@@ -17,8 +17,8 @@ ntiles = (bars + 63) // 64
 e = D.Engine(grid, timing=True)
 e.load_synthetic(0x5EED, 0, S, bars, D.BT_MINUTE)
 e.run(); e.sync()
-buf = (C.c_uint64 * 64)()
-L.bt_read_debug(e._h, buf, 64)
+buf = (C.c_uint64 * 80)()
+L.bt_read_debug(e._h, buf, 80)
 roles = (("param waves", "helper A (scan)", "helper B (chain)", "task waves") if cfg == 3 else
          ("param wave 0", "param wave 1", "param wave 2", "param wave 3+", "helper (scan)", "task waves",
           "accountant"))
@@ -27,7 +27,8 @@ for role, who in enumerate(roles):
     w, b = buf[8 * role] / n / ntiles, buf[8 * role + 1] / n / ntiles
     x = [buf[8 * role + 2 + i] / n / ntiles for i in range(4)]
     print(f"config {cfg} {who:18s} waves {buf[8*role+7]:6d}  work {w:7.0f}  barrier {b:7.0f} cyc/tile"
-          f"  [setup {x[0]:.0f} walk {x[1]:.0f} tile-end {x[2]:.0f} iters {x[3]:.2f}]")
+          f"  [setup {x[0]:.0f} walk {x[1]:.0f} tile-end {x[2]:.0f} iters {x[3]:.2f}]"
+          + (f" tasks: words {buf[8 * role + 6] / n / ntiles:.0f} levels {buf[64 + role] / n / ntiles:.0f}" if cfg == 4 else ""))
 if cfg == 4:
     ids = [buf[56 + w] - 1 for w in range(8) if buf[56 + w]]
     print("block 0 hardware waves: SIMD", [(i >> 4) & 3 for i in ids], "wave slot", [i & 15 for i in ids], "CU", [(i >> 8) & 15 for i in ids])
