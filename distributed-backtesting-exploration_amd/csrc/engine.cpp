@@ -242,9 +242,15 @@ void upload_grid(bt_engine* e) {
 
 int64_t align_rows(int64_t bars) { return (bars + kRowAlign - 1) / kRowAlign * kRowAlign; }
 
+void sync_all(bt_engine* e);
+
 // Install a dataset: symbol descriptors (row offsets into the columns) and `rows` rows per
 // column; allocates the columns the strategy needs.
 void set_dataset(bt_engine* e, std::vector<SymDesc>&& syms, int64_t rows) {
+    // the previous run's top-k chain (second stream) reads the symbol descriptors (ids of its
+    // records), and a column may be reallocated below: both streams drain first (the upload on
+    // the engine stream alone would be ordered after the kernel but not after that chain)
+    sync_all(e);
     e->syms = std::move(syms);
     e->rows = rows;
     const size_t n_sym = e->syms.size();

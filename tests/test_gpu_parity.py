@@ -317,7 +317,10 @@ def test_spec_maximum_windows(strategy):
 
 def test_pipelined_topk_fetch():
     """bench.py's pipelining: run i+1 is enqueued before run i's top-k is read; each slot must
-    hold its own run's records and trade count (same as the synchronous read of that run)."""
+    hold its own run's records and trade count (same as the synchronous read of that run).
+    Reloading the data between the runs must not race the previous run's top-k chain, which
+    reads the symbol descriptors on the second stream (round 2: a reload overwrote them first
+    and slot 0 reported symbol 305 for 5); repeated, since a race shows only sometimes."""
     grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
     with D.Engine(grid, topk=20) as e:
         refs = []
@@ -325,15 +328,16 @@ def test_pipelined_topk_fetch():
             e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
             e.run()
             refs.append((e.read_topk(), e.stats()["trades"]))
-        e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
-        e.run()
-        e.topk_fetch_async(0)
-        e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)   # stream-ordered after slot 0's copy
-        e.run()
-        e.topk_fetch_async(1)
-        for slot, (top, trades) in enumerate(refs):
-            got, n = e.topk_fetch_wait(slot)
-            assert got.tolist() == top.tolist() and n == trades
+        for _ in range(6):
+            e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
+            e.run()
+            e.topk_fetch_async(0)
+            e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)   # drains the top-k chain of slot 0 first
+            e.run()
+            e.topk_fetch_async(1)
+            for slot, (top, trades) in enumerate(refs):
+                got, n = e.topk_fetch_wait(slot)
+                assert got.tolist() == top.tolist() and n == trades
 
 
 @pytest.mark.parametrize("hi_prices", [False, True])
