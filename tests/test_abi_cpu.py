@@ -150,3 +150,43 @@ def test_result_lines_match_printf_format():
                % (p, r["n_trades"], r["pnl"], r["mdd"], r["exposure"], r["sharpe"], r["hash"]))
         assert line == exp, (p, line, exp)
         assert json.loads(line)["param"] == p
+
+
+def build_abi_host(tmpdir):
+    """tests/abi_host.c — a compiled C99 host of include/bt.h (what a Rust / C worker links):
+    built with -std=c99 -pedantic -Werror against the in-tree libbt.so."""
+    exe = os.path.join(str(tmpdir), "abi_host")
+    lib_dir = os.path.dirname(E.LIB_PATH)
+    r = subprocess.run(["gcc", "-std=c99", "-pedantic", "-Wall", "-Wextra", "-Werror",
+                        "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "abi_host.c"),
+                        "-L", lib_dir, "-l:" + os.path.basename(E.LIB_PATH),
+                        "-Wl,-rpath," + lib_dir, "-Wl,-rpath-link,/opt/rocm/lib", "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_c99_host_compiles_and_struct_layouts_match_the_python_mirror(tmp_path):
+    """bt.h is plain C99 (a Rust / C host binds it as is), and every struct the Python mirror
+    (engine.py ctypes classes and numpy dtypes) reads has the header's size and offsets."""
+    exe = build_abi_host(tmp_path)
+    got = json.loads(subprocess.run([exe, "layout"], capture_output=True, text=True, check=True).stdout)
+    assert got["abi_version"] == 1
+    mirror = {"bt_config": E._Config, "bt_job_in": E._JobIn, "bt_job_out": E._JobOut,
+              "bt_batch_profile": E._BatchProfile, "bt_stats": E._Stats}
+    for cname, cls in mirror.items():
+        assert got[cname] == C.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            key = f"{cname}.{f}"
+            if key in got:
+                assert got[key] == getattr(cls, f).offset, key
+    dtypes = {"bt_summary": E.SUMMARY_DTYPE, "bt_trade": E.TRADE_DTYPE, "bt_sums": E.SUMS_DTYPE,
+              "bt_topk_rec": E.TOPK_DTYPE}
+    for cname, dt in dtypes.items():
+        assert got[cname] == dt.itemsize, cname
+        for f in dt.names:
+            key = f"{cname}.{f}"
+            if key in got:
+                assert got[key] == dt.fields[f][1], key
+    checked = [k for k in got if "." in k]
+    assert len(checked) >= 30
