@@ -72,6 +72,8 @@ uint32_t next_pow2(uint32_t x) {
 
 void bt::set_last_error(const std::string& s) { set_err(s); }
 
+constexpr int64_t kNtrRing = 64;  // per-run trade counter slots (bt_engine::d_ntr_ring)
+
 struct bt_engine {
     bt_config cfg{};
     std::vector<int32_t> ax[4];  // owned copies of the grid axes
@@ -89,7 +91,12 @@ struct bt_engine {
     // (on tstream) still reads the other one; `cur` is the buffer of the last run
     DevBuf<bt_summary> d_sum[2];
     DevBuf<uint64_t> d_key[2];
-    DevBuf<unsigned long long> d_ntr[2];
+    // per-run trade counters: a ring of kNtrRing slots, run r accumulating into slot
+    // r % kNtrRing; half the ring is zeroed every kNtrRing / 2 runs (slots last used >= 33 runs
+    // earlier), so a run enqueues no memset of its own. ntr[b]: the slot of the last run that
+    // wrote output buffer b
+    DevBuf<unsigned long long> d_ntr_ring;
+    unsigned long long* ntr[2] = {nullptr, nullptr};
     int cur = 0;
     int64_t nrun = 0;
     DevBuf<bt_sums> d_sums;
@@ -305,8 +312,8 @@ void ensure_outputs(bt_engine* e) {
     for (int b = 0; b < 2; ++b) {
         e->d_sum[b].ensure(std::max<size_t>(1, n));
         e->d_key[b].ensure(std::max<size_t>(1, n));
-        e->d_ntr[b].ensure(1);
     }
+    e->d_ntr_ring.ensure(kNtrRing);
     if (e->cfg.flags & BT_FLAG_PARITY) {
         e->d_sums.ensure(std::max<size_t>(1, n));
         e->d_trades.ensure(std::max<size_t>(1, n * (size_t)e->cfg.trade_cap));
@@ -328,10 +335,13 @@ void run_impl(bt_engine* e) {
     activate(e);
     ensure_outputs(e);
     const int32_t S = (int32_t)e->syms.size();
-    const int b = (int)(e->nrun++ & 1);
+    const int64_t run = e->nrun++;
+    const int b = (int)(run & 1);
     e->cur = b;
-    // buffer b was last read by the top-k chain / read-back of run i-2: wait for them
-    if (e->tdone_armed[b]) HIPCHK(hipStreamWaitEvent(e->stream, e->ev_tdone[b], 0));
+    // buffer b was last read by the top-k chain / read-back of run i-2: wait for them (no wait
+    // packet when they have already finished, the steady state of a pipelined sweep)
+    if (e->tdone_armed[b] && hipEventQuery(e->ev_tdone[b]) != hipSuccess)
+        HIPCHK(hipStreamWaitEvent(e->stream, e->ev_tdone[b], 0));
     Out out{};
     out.sum = e->d_sum[b].p;
     out.key = e->d_key[b].p;
@@ -339,8 +349,12 @@ void run_impl(bt_engine* e) {
     out.sums = parity ? e->d_sums.p : nullptr;
     out.trades = parity ? e->d_trades.p : nullptr;
     out.trade_cap = parity ? e->cfg.trade_cap : 0;
-    out.n_trades = e->d_ntr[b].p;
-    HIPCHK(hipMemsetAsync(e->d_ntr[b].p, 0, sizeof(unsigned long long), e->stream));
+    const int slot = (int)(run % kNtrRing);
+    if (slot % (kNtrRing / 2) == 0)
+        HIPCHK(hipMemsetAsync(e->d_ntr_ring.p + slot, 0, (kNtrRing / 2) * sizeof(unsigned long long),
+                              e->stream));
+    e->ntr[b] = e->d_ntr_ring.p + slot;
+    out.n_trades = e->ntr[b];
     out.dbg = nullptr;
     if (BT_ABL(e->grid, 64)) {  // profiling stamps (profiling build only)
         e->d_dbg.ensure(80);
@@ -412,8 +426,10 @@ void run_impl(bt_engine* e) {
         e->ev_pending.push_back(ev);
     }
     if (e->cfg.topk > 0) {
-        HIPCHK(hipEventRecord(e->ev_kdone, e->stream));
-        HIPCHK(hipStreamWaitEvent(e->tstream, e->ev_kdone, 0));
+        // the chain waits for the kernel: on the timing end event when there is one (one
+        // marker less between two runs' kernels)
+        if (!timing) HIPCHK(hipEventRecord(e->ev_kdone, e->stream));
+        HIPCHK(hipStreamWaitEvent(e->tstream, timing ? ev.second : e->ev_kdone, 0));
         HIPCHK(launch_topk(e->d_key[b].p, e->d_sum[b].p, e->d_syms.p, (int64_t)S * e->P, e->P,
                            e->cfg.topk, topk_work(e), e->tstream));
         HIPCHK(hipEventRecord(e->ev_tdone[b], e->tstream));
@@ -712,7 +728,7 @@ bool bt::engine_exchange_view(bt_engine* e, ExchangeView& v, std::string& err) {
     v.device = e->cfg.device;
     v.topk = e->cfg.topk;
     v.d_top = e->d_top.p;
-    v.d_ntr = e->d_ntr[e->cur].p;
+    v.d_ntr = e->ntr[e->cur];
     v.bar_evals = 0;
     for (const SymDesc& s : e->syms) v.bar_evals += (int64_t)s.bars * e->P;
     return true;
@@ -817,13 +833,13 @@ void bt_engine_destroy(bt_engine* e) {
         for (int b = 0; b < 2; ++b) {
             e->d_sum[b].release();
             e->d_key[b].release();
-            e->d_ntr[b].release();
             if (e->ev_tdone[b]) (void)hipEventDestroy(e->ev_tdone[b]);
             e->ev_tdone[b] = nullptr;
             e->tdone_armed[b] = false;
         }
         if (e->ev_kdone) (void)hipEventDestroy(e->ev_kdone);
         e->ev_kdone = nullptr;
+        e->d_ntr_ring.release();
         e->d_sums.release();
         e->d_trades.release();
         e->d_seg.release();
@@ -1010,7 +1026,7 @@ int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot) {
         // complete too (the chain waited for the kernel)
         HIPCHK(hipMemcpyAsync(h, e->d_top.p, ((size_t)e->cfg.topk + 1) * sizeof(bt_topk_rec),
                               hipMemcpyDeviceToHost, e->tstream));
-        HIPCHK(hipMemcpyAsync(h + kTopkMax + 1, e->d_ntr[e->cur].p, sizeof(unsigned long long),
+        HIPCHK(hipMemcpyAsync(h + kTopkMax + 1, e->ntr[e->cur], sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, e->tstream));
         HIPCHK(hipEventRecord(e->slot_ev[slot], e->tstream));
         HIPCHK(hipEventRecord(e->ev_tdone[e->cur], e->tstream));  // buffer readers now end here
@@ -1055,7 +1071,7 @@ int32_t bt_read_stats(bt_engine* e, bt_stats* out) {
         st.errors = e->n_errors;
         if (e->ran) {
             unsigned long long n = 0;
-            HIPCHK(hipMemcpy(&n, e->d_ntr[e->cur].p, sizeof n, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(&n, e->ntr[e->cur], sizeof n, hipMemcpyDeviceToHost));
             st.trades = (int64_t)n;
         }
         *out = st;
