@@ -261,9 +261,14 @@ def main(argv=None):
         paths += sorted(os.path.join(p, f) for f in os.listdir(p)) if os.path.isdir(p) else [p]
     d = Dispatcher(paths, results_path=a.results)
     server, _ = serve(d, a.addr, max_send=a.max_send_mb << 20, gzip=not a.no_gzip)
+    print("dispatcher serving", flush=True)
+    t0 = time.perf_counter()
     try:
         while not (a.exit_when_done and d.all_done()):
-            time.sleep(0.1)
+            time.sleep(0.01 if a.exit_when_done else 0.1)
+        if a.exit_when_done:
+            print(f"dispatcher done {len(d.done_paths)} paths in {time.perf_counter() - t0:.3f} s",
+                  flush=True)
     finally:
         server.stop(1)
         d.close()

@@ -216,9 +216,16 @@ class Worker:
                 if now >= next_job:
                     self.handle_job()
                     next_job = now + self.job_tick
-                try:  # main.rs:80-83
+                # main.rs:80-83: a completion is sent as soon as it is ready (the select loop
+                # takes ready completions between ticks), so every queued one goes now
+                try:
                     jid, data = self.complete_q.get(timeout=0.01)
-                    self._complete(P.CompleteRequest(id=jid, data=data))
+                    while True:
+                        try:
+                            self._complete(P.CompleteRequest(id=jid, data=data))
+                        except grpc.RpcError as why:  # the reference unwraps (panics) here
+                            log.error("Unable to complete %s: %s", jid, why)
+                        jid, data = self.complete_q.get_nowait()
                 except queue.Empty:
                     pass
         finally:
@@ -230,10 +237,13 @@ class Worker:
 
 
 def main(argv=None):
-    from .engine import BT_BOLL, BT_EMA_OLS, Engine, config2_grid, config3_grid, config4_grid
+    from .engine import Engine, config2_grid, config3_grid, config4_grid, config5_grid
     ap = argparse.ArgumentParser(description="GPU worker for the backtesting dispatcher")
     ap.add_argument("--target", default="[::1]:50051")            # main.rs:48
     ap.add_argument("--strategy", default="sma", choices=["sma", "ema_ols", "boll"])
+    ap.add_argument("--grid", default=None, choices=["config2", "config3", "config4", "config5"],
+                    help="a BASELINE config's parameter grid (overrides --strategy)")
+    ap.add_argument("--quiet", action="store_true", help="log warnings only")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--cores", type=int, default=None, help="jobs per RequestJobs")
     ap.add_argument("--max-receive-mb", type=int, default=4)
@@ -244,13 +254,19 @@ def main(argv=None):
     ap.add_argument("--fetchers", type=int, default=1,
                     help="RequestJobs connections kept busy (1: the reference's job tick only)")
     ap.add_argument("--duration", type=float, default=None)
+    ap.add_argument("--job-tick", type=float, default=0.250,
+                    help="seconds between RequestJobs on the main connection (main.rs:68)")
     a = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO)
-    grid = {"sma": config2_grid, "ema_ols": config3_grid, "boll": config4_grid}[a.strategy]()
+    logging.basicConfig(level=logging.WARNING if a.quiet else logging.INFO)
+    grids = {"config2": config2_grid, "config3": config3_grid, "config4": config4_grid,
+             "config5": config5_grid}
+    grid = grids[a.grid]() if a.grid else \
+        {"sma": config2_grid, "ema_ols": config3_grid, "boll": config4_grid}[a.strategy]()
     eng = Engine(grid, device=a.device)
+    print("worker ready", flush=True)
     Worker(a.target, engine_processor(eng), a.cores,
            max_receive=a.max_receive_mb << 20, max_batch_bytes=a.max_batch_mb << 20,
-           min_batch_jobs=a.min_batch_jobs, fetchers=a.fetchers).run(a.duration)
+           min_batch_jobs=a.min_batch_jobs, fetchers=a.fetchers, job_tick=a.job_tick).run(a.duration)
 
 
 if __name__ == "__main__":
