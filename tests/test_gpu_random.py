@@ -5,6 +5,8 @@ The price paths are chosen to reach the kernels' rare branches: narrow integer w
 floor keys, exact SMA ties, flat stretches), plateaus, spikes near the 2^31-tick ceiling, and
 lengths that end mid-tile, exactly on a tile edge or before the longest window fills.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -14,6 +16,8 @@ from helpers import compare_summary, compare_trades, oracle_row
 pytestmark = pytest.mark.gpu
 
 CAP = 4096
+# seeds per sweep (BT_RANDOM_SEEDS widens a sweep for a one-off deep run)
+NS = int(os.environ.get("BT_RANDOM_SEEDS", "0"))
 
 
 def _series(rng, n, kind):
@@ -39,7 +43,7 @@ def _windows(rng, k, top):
     return sorted(set(int(x) for x in rng.integers(1, top, k)))
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(NS or 12))
 def test_random_sma(seed):
     rng = np.random.default_rng(1000 + seed)
     grid = D.Grid.sma(_windows(rng, 7, 40), _windows(rng, 6, 300), annualization=252)
@@ -58,7 +62,7 @@ def test_random_sma(seed):
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
-@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("ema_ols", "boll") for s in range(5)])
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("ema_ols", "boll") for s in range(NS or 5)])
 def test_random_tile_strategies(strategy, seed):
     rng = np.random.default_rng(2000 + seed + (100 if strategy == "boll" else 0))
     if strategy == "ema_ols":
@@ -82,3 +86,35 @@ def test_random_tile_strategies(strategy, seed):
             where = f"{strategy} seed {seed} sym {s} len {len(cl)} {grid.param(p)}"
             compare_summary(got[s, p], orc[p], where)
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("sma", "ema_ols", "boll")
+                                           for s in range(NS or 4)])
+def test_random_product_kernels(strategy, seed):
+    """The release instantiations (no trade lists: the split Bollinger walk, the SMA kernel's
+    fast paths) on the same kinds of random grids and paths, every summary field vs the oracle."""
+    rng = np.random.default_rng(3000 + seed + 100 * ("sma", "ema_ols", "boll").index(strategy))
+    if strategy == "sma":
+        grid = D.Grid.sma(_windows(rng, 7, 40), _windows(rng, 6, 300), annualization=252)
+    elif strategy == "ema_ols":
+        grid = D.Grid.ema_ols(_windows(rng, 4, 200), _windows(rng, 4, 400),
+                              band_bps=int(rng.integers(0, 60)))
+    else:
+        # 64 lanes per k value (8 windows x 2 x 4 levels), as config 4: the launcher splits the
+        # walk of the smallest k's wave into a finder and an accountant
+        pick = lambda lo, hi, k: sorted(int(x) for x in rng.choice(np.arange(lo, hi), k, replace=False))
+        grid = D.Grid.boll(pick(2, 121, 8), pick(1, 9, 4), pick(10, 300, 2), pick(10, 500, 4), k_den=2)
+    kinds = ["walk", "narrow", "plateau", "spiky"]
+    closes = [_series(rng, int(n), kinds[i % 4])
+              for i, n in enumerate(rng.choice([1, 2, 64, 65, 129, 500, 2000, 3000], 8))]
+    highs, lows = zip(*[_ohlc(rng, c) for c in closes])
+    ann = 252 if strategy == "sma" else 98280
+    with D.Engine(grid) as e:
+        e.load_ohlc(closes, list(highs), list(lows))
+        e.run()
+        got = e.summaries()
+    for s, cl in enumerate(closes):
+        ohlc = (cl, cl, cl, cl) if strategy == "sma" else (cl, highs[s], lows[s], cl)
+        orc, _ = oracle_row(strategy, grid, ohlc, ann, CAP)
+        for p in range(grid.n_params):
+            compare_summary(got[s, p], orc[p], f"{strategy} seed {seed} sym {s} len {len(cl)} {grid.param(p)}")
