@@ -150,3 +150,37 @@ def test_ema_auto_split_config3_grid_small_shard():
         orc, _ = oracle_row("ema_ols", grid, (o, h, lo, c), 98280)
         for p in range(0, grid.n_params, 3):
             compare_summary(got[s, p], orc[p], f"ema auto split sym {200 + s} {grid.param(p)}")
+
+
+_NS = int(__import__("os").environ.get("BT_RANDOM_SEEDS", "0"))
+
+
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("boll", "ema_ols") for s in range(_NS or 3)])
+def test_random_splits_equal_unsplit(strategy, seed):
+    """Random grids, segment counts (2-6), burn-ins (1-6 tiles) and ragged random-walk series:
+    the split run equals the unsplit one bit for bit (the unsplit kernels are oracle-checked by
+    the parity sweeps), whether or not the fix pass re-walks boundaries."""
+    rng = np.random.default_rng(4000 + seed + (500 if strategy == "ema_ols" else 0))
+    pick = lambda lo, hi, k: sorted(int(x) for x in rng.choice(np.arange(lo, hi), k, replace=False))
+    if strategy == "boll":
+        grid = D.Grid.boll(pick(2, 121, 8), pick(1, 9, 4), pick(10, 300, 2), pick(10, 500, 4), k_den=2)
+    else:
+        grid = D.Grid.ema_ols(pick(2, 200, 4), pick(2, 400, 4), band_bps=int(rng.integers(0, 60)))
+    n = int(rng.integers(2, 6))
+    closes, highs, lows = [], [], []
+    for i in range(n):
+        bars = int(rng.integers(1, 16000))
+        c = np.clip(1_000_000 + np.cumsum(rng.integers(-3000, 3001, bars)), 10_000, 2**31 - 1)
+        closes.append(c.astype(np.int32))
+        highs.append(np.clip(c + rng.integers(0, 2000, bars), 1, 2**31 - 1).astype(np.int32))
+        lows.append(np.clip(c - rng.integers(0, 2000, bars), 1, 2**31 - 1).astype(np.int32))
+    G, burn = int(rng.integers(2, 7)), int(rng.integers(1, 7))
+    outs = []
+    for segments, b in ((1, 0), (G, burn)):
+        with D.Engine(grid) as e:
+            e.set_segments(segments, b)
+            e.load_ohlc(closes, highs, lows)
+            e.run()
+            outs.append(e.summaries().copy())
+            assert e.last_segments() == segments
+    assert outs[1].tobytes() == outs[0].tobytes(), f"{strategy} G={G} burn={burn}"
