@@ -513,3 +513,24 @@ def test_torch_nccl_backend_exchange_world1():
         comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_run_batch_empty_all_failed_then_good():
+    """An empty JobsReply, then one whose every job is malformed (no kernel launch, every job
+    answered with an error), then a good one on the same engine: results stay exact."""
+    import json
+    import oracle_np as N
+    grid = D.Grid.sma([4, 10], [50, 120], annualization=252)
+    o, h, lo, c, v = N.gen(0x5EED, [5], 700, 0)
+    good = N.csv_bytes(o[0], h[0], lo[0], c[0], v[0], 0)
+    with D.Engine(grid) as e:
+        assert e.run_batch([]) == []
+        bad = e.run_batch([("a", b""), ("b", b"not,a,csv\n"), ("c", b"DBXCOL1\n\x00\x00")])
+        assert all(st < 0 and "error" in json.loads(d) for st, d in bad)
+        (st, data), = e.run_batch([("g", good)])
+    assert st == 0
+    orc, _ = oracle_row("sma", grid, (c[0], c[0], c[0], c[0]), 252)
+    for p, line in enumerate(data.strip().split("\n")):
+        j = json.loads(line)
+        assert j["n"] == int(orc[p]["n_trades"]) and j["pnl"] == int(orc[p]["pnl"])
+        assert int(j["h"], 16) == int(orc[p]["hash"])
