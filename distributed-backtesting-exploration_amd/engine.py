@@ -7,8 +7,10 @@ there is no CPU fallback: if libbt.so or a GPU is missing, constructing an Engin
 from __future__ import annotations
 
 import ctypes as C
+import importlib.util
 import os
 import subprocess
+import sys
 from dataclasses import dataclass, field
 from typing import Sequence
 
@@ -90,12 +92,25 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def _one_hip_runtime():
+    """libbt.so needs libamdhip64.so.7 by SONAME. PyTorch-ROCm loads its bundled HIP and HSA
+    runtimes by path, so a process that loads libbt.so first and torch afterwards holds two HSA
+    runtimes, and torch then finds no GPU ("No HIP GPUs are available"; measured on the MI355X,
+    scripts/dev/torch_after_libbt.py). With torch installed, importing it first lets libbt.so bind
+    torch's copy: one runtime per process, whatever the caller imports later."""
+    if "torch" in sys.modules:
+        return
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def lib():
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise BtError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback)")
+    _one_hip_runtime()
     L = C.CDLL(LIB_PATH)
     P = C.c_void_p
     L.bt_engine_create.argtypes = [C.POINTER(_Config), C.c_char_p, C.c_size_t]
