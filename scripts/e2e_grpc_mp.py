@@ -75,8 +75,12 @@ def main():
         workers.append(p)
         threading.Thread(target=_lines, args=(p, wout), daemon=True).start()
     t_ready = time.perf_counter()
+    beat = t_ready
     while sum(1 for _, ln in wout if ln == "worker ready") < a.workers:
-        if time.perf_counter() - t_ready > 90 or any(p.poll() is not None for p in workers):
+        if time.perf_counter() - beat > 20:  # the first torch import on a fresh box takes minutes
+            beat = time.perf_counter()
+            print(f"  ... waiting for workers ({time.perf_counter() - t_ready:.0f} s)", flush=True)
+        if time.perf_counter() - t_ready > 240 or any(p.poll() is not None for p in workers):
             for p in workers:
                 p.kill()
             raise SystemExit("workers did not start: " + "\n".join(ln for _, ln in wout[-20:]))
