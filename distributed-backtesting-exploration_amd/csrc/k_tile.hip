@@ -168,6 +168,17 @@ __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
 // Bits [cur, 63] of a tile word (none for cur >= 64).
 __device__ __forceinline__ uint64_t bits_from(int cur) { return cur < kTile ? (~0ULL << cur) : 0ULL; }
 
+// State after every bar of a tile of a set/reset latch (set S and reset R disjoint), q = the
+// state before bar 0: an add with carry, whose carry out of bit b is S_b | (~R_b & carry into b).
+__device__ __forceinline__ uint64_t latch64(uint64_t S, uint64_t R, uint64_t q) {
+    const uint64_t A = ~R;
+    const uint64_t s1 = A + S;
+    uint64_t cout = s1 < A;
+    const uint64_t sum = s1 + q;
+    cout |= sum < s1;
+    return ((sum ^ A ^ S) >> 1) | (cout << 63);
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- EMA + OLS
@@ -420,44 +431,65 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             const uint64_t Xw = W[4 * i_n + 2] & vm, Yw = W[4 * i_n + 3] & vm;
             const int bl = B - 1 - t0;
             const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;  // forced exit (bl >= 0)
-            int cur = 0;
-            // one trade (entry and/or exit) per call, in bar order; false when the tile is done.
-            // Only the first trade of the tile can start open (a position carried in, path in
-            // a.agg): later ones start flat and their path lies in this tile (no merge)
-            auto trade = [&](auto first_tag) -> bool {
-                constexpr bool FIRST = decltype(first_tag)::value;
-                if (STAMPS) sa.count(3);
-                if (!FIRST || a.pos == 0) {
-                    const uint64_t m = (Aw | Bw) & bits_from(cur);
-                    if (m == 0) return false;
-                    const int b = __builtin_ctzll(m);
-                    const int np = ((Aw >> b) & 1) ? 1 : -1;
-                    const int32_t cx = cT[b];
-                    const uint64_t qx = (uint64_t)ql[b], q2x = (uint64_t)ql[kTile + b];
-                    a.ps1 += np > 0 ? (uint64_t)0 - qx : qx;
-                    a.ps2 -= q2x;
-                    acct_open(a, t0 + b, b, cx);
-                    a.pos = np;
-                    cur = b + 1;
-                }
-                const uint64_t m = ((a.pos > 0 ? Xw : Yw) | fb) & bits_from(cur);
-                if (m == 0) return false;
-                const int x = __builtin_ctzll(m);
-                const int32_t cx = cT[x];
-                const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                const Agg seg = dst_query_bf(D, a.sb, x);
-                const Agg st = FIRST ? agg_merge(a.agg, seg) : seg;
-                const bool lg = a.pos > 0;
-                acct_close<PARITY, SEG>(a, t0 + x, cx, st, tr, cap);
-                a.ps1 += lg ? qx : (uint64_t)0 - qx;
-                a.ps2 += q2x;
-                a.pos = 0;
-                cur = x + 1;
-                return true;
-            };
-            if (trade(std::true_type{})) {
+            // positions after every bar at once (replaces a per-trade search for the next entry
+            // and exit bar): a long latch (set A, reset X or the forced exit) and a short one (set
+            // B, reset Y); A and X are disjoint, B and Y too (band >= 0 and e > 0, so a close under
+            // the lower band is under the EMA, fp64 rounding being monotone).
+            // They are coupled only through "an entry needs a flat position": an entry bit
+            // survives if the other side was not held before that bar. Bit b of the coupled masks
+            // depends only on bits < b, so iterating to the fixpoint settles one more bar per pass
+            // at least (one or two passes in practice).
+            {
+                const uint64_t RL = Xw | fb, RS = Yw | fb;
+                const uint64_t lin = a.pos > 0, sin = a.pos < 0;
+                uint64_t Ap = Aw, Bp = Bw, Lw, Sw;
 #pragma unroll 1
-                while (trade(std::false_type{})) {
+                for (;;) {
+                    Lw = latch64(Ap, RL, lin);
+                    Sw = latch64(Bp, RS, sin);
+                    const uint64_t An = Aw & ~((Sw << 1) | sin), Bn = Bw & ~((Lw << 1) | lin);
+                    if (An == Ap && Bn == Bp) break;
+                    Ap = An;
+                    Bp = Bn;
+                }
+                const uint64_t Lb = (Lw << 1) | lin, Sb = (Sw << 1) | sin;
+                const uint64_t EL = Lw & ~Lb;
+                uint64_t Ev = EL | (Sw & ~Sb), Xv = (Lb & ~Lw) | (Sb & ~Sw);
+                if (a.pos != 0 && Xv) {  // the position carried in closes first
+                    const int x = __builtin_ctzll(Xv);
+                    Xv &= Xv - 1;
+                    const int32_t cx = cT[x];
+                    const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                    const bool lg = a.pos > 0;
+                    acct_close<PARITY, SEG>(a, t0 + x, cx, agg_merge(a.agg, dst_query_bf(D, a.sb, x)), tr, cap);
+                    a.ps1 += lg ? qx : (uint64_t)0 - qx;
+                    a.ps2 += q2x;
+                    a.pos = 0;
+                }
+#pragma unroll 1
+                while (Ev) {
+                    if (STAMPS) sa.count(3);
+                    // entry and exit bars are both known: every LDS read of the trade is issued
+                    // together (an entry left open reads the tile's last bar, unused)
+                    const int b = __builtin_ctzll(Ev);
+                    Ev &= Ev - 1;
+                    const bool hx = Xv != 0;
+                    const int x = hx ? __builtin_ctzll(Xv) : kTile - 1;
+                    Xv &= Xv - 1;
+                    const int32_t cb = cT[b], cx = cT[x];
+                    const uint64_t qb = (uint64_t)ql[b], q2b = (uint64_t)ql[kTile + b];
+                    const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                    const Agg st = dst_query_bf(D, b, x);
+                    const int np = ((EL >> b) & 1) ? 1 : -1;
+                    a.ps1 += np > 0 ? (uint64_t)0 - qb : qb;
+                    a.ps2 -= q2b;
+                    acct_open(a, t0 + b, b, cb);
+                    a.pos = np;
+                    if (!hx) break;  // open at the tile end
+                    acct_close<PARITY, SEG>(a, t0 + x, cx, st, tr, cap);
+                    a.ps1 += np > 0 ? qx : (uint64_t)0 - qx;
+                    a.ps2 += q2x;
+                    a.pos = 0;
                 }
             }
             if (STAMPS) sa.mark(1);
