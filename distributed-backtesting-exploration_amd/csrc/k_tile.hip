@@ -188,8 +188,9 @@ __device__ __forceinline__ uint64_t latch64(uint64_t S, uint64_t R, uint64_t q) 
 //   every wave, tile k+1, after its own work: condition words, one task per span (4 ballots
 //           over the EMA values) or per OLS window (exact numerator sign), grabbed from an LDS
 //           counter;
-//   parameter waves, tile k: one trade per loop iteration (entry at the first entry bar, exit
-//           at the first exit bar), O(1) accounting per trade.
+//   parameter waves, tile k: the position after every bar from two coupled set/reset latches
+//           over the condition words (latch64), then one trade per loop iteration over the
+//           latches' edges, O(1) accounting per trade.
 // SEG: bar segments as in boll_tile_kernel; besides the lanes' trade states a segment's start
 // must agree on the EMA chains: a speculative segment starts each chain at its first scanned bar
 // (e = c there) and records the values entering its first accounted bar; fp64 chains from
