@@ -890,51 +890,75 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const uint64_t S1 = P1t - r1[pj];
             const unsigned __int128 S2 = P2t - r2[pj];
             const int64_t Dv = (int64_t)Wn * c - (int64_t)S1;
-            const unsigned __int128 Q = mul_u128_u32(S2, (uint32_t)Wn) - sq_u64(S1);  // >= 0 on valid bars
-            // fp64 fast path: |z| > k <=> Dv^2 kd^2 > kn^2 Q. |Dv| < 2^53 converts exactly; lh and
-            // rh = kn^2 Q (Q < 2^87: (Q >> 32) < 2^55 rounds once, the low word once more, the
-            // product once) are within 2^-50 relative of the exact sides. lhd = lh (1 - 2^-48) > rh
-            // then proves L > R and lhu = lh (1 + 2^-48) < rh proves L < R; a valid lane with
-            // neither (both sides zero included) is settled exactly in int128 with its whole wave.
+            // Q = W S2 - S1^2 in fp64 with a proven bracket: S1 < 2^44 converts exactly, S2 <
+            // 2^75 rounds once, the product, the square and the difference once each, and S1^2 <=
+            // W S2, so |Qd - Q| < 2^-50 pd (pd = W S2 rounded). Qd -/+ 2^-48 pd then brackets Q
+            // with room for the roundings of the bracket and of the k^2 products below.
+            const double S2d = (double)(uint64_t)(S2 >> 32) * 0x1p32 + (double)(uint32_t)S2;
+            const double S1d = (double)S1;
+            const double pd = (double)Wn * S2d;
+            const double Qd = pd - S1d * S1d;
+            // with lh's own margin folded in (lh is within 2^-51 of L; 2^-47 covers both)
+            const double QH = (Qd + pd * 0x1p-48) * (1.0 + 0x1p-47);
+            const double QL = (Qd - pd * 0x1p-48) * (1.0 - 0x1p-47);
+            // fp64 fast path: |z| > k <=> L = Dv^2 kd^2 > R = kn^2 Q. |Dv| < 2^53 converts exactly
+            // and lh is within 2^-51 of L; after rounding lh > kn^2 QH proves L > R and
+            // kn^2 QL > lh proves L < R. A valid lane with neither (both sides zero included, or a
+            // window so flat that Q is inside the bracket) is settled exactly in int128 with its
+            // whole wave.
             const double Dd = (double)Dv;
             const double lh = (Dd * Dd) * kd2d;
-            const double lhd = lh * (1.0 - 0x1p-48), lhu = lh * (1.0 + 0x1p-48);
-            const double Qd = (double)(uint64_t)(Q >> 32) * 0x1p32 + (double)(uint32_t)Q;
             const uint64_t vm = ballot(valid);
             const uint64_t dp = ballot(valid && Dv >= 0), dn = ballot(valid && Dv <= 0);
             const uint64_t zneg = vm & ~dp, zpos = vm & ~dn;  // Dv < 0, Dv > 0
-            // the z words of one k: lane 0 .. 4 kMaxK - 1 of `zw` collect them (v_writelane, lane
-            // = dword of Wd[2 (ow nk + q) + side]), one store per pass of kMaxK values
-            auto ztest = [&](auto qtag, int q, double kn2, uint32_t& zw) {
+            // z tests of one k: lane 4 qq .. 4 qq + 3 of `zw` collect its words (v_writelane, lane
+            // = dword of Wd[2 (ow nk + q) + side]), one store per pass of kMaxK values; a
+            // lane the fp64 bracket cannot settle marks the k in `unc` (wave-uniform), and the
+            // pass then settles those k exactly in int128, once, outside the unrolled tests
+            auto ztest = [&](auto qtag, double kn2, uint32_t& zw, uint32_t& unc) {
                 constexpr int qq = decltype(qtag)::value;
-                const double rh = kn2 * Qd;
-                uint64_t big = vcmp_gt_f64(lhd, rh) & vm;
-                const uint64_t small = vcmp_gt_f64(rh, lhu);
-                if (vm & ~big & ~small) {  // rare: settle the whole wave exactly in int128
-                    const int64_t kn = g.b[q];
-                    big = sgpr64(ballot(valid && (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * (i128)Q));
-                }
+                const uint64_t big = vcmp_gt_f64(lh, kn2 * QH) & vm;
+                const uint64_t small = vcmp_gt_f64(kn2 * QL, lh);
+                if (vm & ~big & ~small) unc |= 1u << qq;
                 const uint64_t zl = big & zneg, zh = big & zpos;
                 writelane<4 * qq>(zw, (uint32_t)zl);
                 writelane<4 * qq + 1>(zw, (uint32_t)(zl >> 32));
                 writelane<4 * qq + 2>(zw, (uint32_t)zh);
                 writelane<4 * qq + 3>(zw, (uint32_t)(zh >> 32));
             };
+            auto settle = [&](int q0, uint32_t unc, uint32_t& zw) {  // rare
+                const uint64_t S1x = P1t - r1[pj];
+                const unsigned __int128 S2x = P2t - r2[pj];
+                const unsigned __int128 Q = mul_u128_u32(S2x, (uint32_t)Wn) - sq_u64(S1x);
+#pragma unroll 1
+                while (unc) {
+                    const int qq = __builtin_amdgcn_readfirstlane(__builtin_ctz(unc));
+                    unc &= unc - 1;
+                    const int64_t kn = g.b[q0 + qq];
+                    const uint64_t big = sgpr64(ballot(valid && (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * (i128)Q));
+                    const uint64_t zl = big & zneg, zh = big & zpos;
+                    const int d = lane - 4 * qq;  // lane 4 qq + d holds dword d of (zl, zh)
+                    if (d >= 0 && d < 4)
+                        zw = (uint32_t)((d < 2 ? zl : zh) >> (32 * (d & 1)));
+                }
+            };
             {  // first pass: k_num^2 from the kernel arguments
-                uint32_t zw = 0;
+                uint32_t zw = 0, unc = 0;
                 static_for<kMaxK>([&](auto qtag) {
                     constexpr int qq = decltype(qtag)::value;
-                    if (qq < nk) ztest(qtag, qq, g.kn2[qq], zw);
+                    if (qq < nk) ztest(qtag, g.kn2[qq], zw, unc);
                 });
+                if (unc) settle(0, unc, zw);
                 if (lane < 4 * min(nk, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * ow * nk)[lane] = zw;
             }
 #pragma unroll 1
             for (int q0 = kMaxK; q0 < nk; q0 += kMaxK) {  // grids of more than 8 k values
-                uint32_t zw = 0;
+                uint32_t zw = 0, unc = 0;
                 static_for<kMaxK>([&](auto qtag) {
                     constexpr int qq = decltype(qtag)::value;
-                    if (q0 + qq < nk) ztest(qtag, q0 + qq, kn2d[q0 + qq], zw);
+                    if (q0 + qq < nk) ztest(qtag, kn2d[q0 + qq], zw, unc);
                 });
+                if (unc) settle(q0, unc, zw);
                 if (lane < 4 * min(nk - q0, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * (ow * nk + q0))[lane] = zw;
             }
             if (lane == 0) {
