@@ -460,22 +460,9 @@ std::vector<bt_topk_rec> read_topk_impl(bt_engine* e, int32_t k) {
     sync_all(e);
     int32_t n = 0;
     memcpy(&n, e->h_top, sizeof n);
-    std::vector<bt_topk_rec> res;
-    if (n >= 0) {
-        res.assign(e->h_top + 1, e->h_top + 1 + n);
-    } else {  // more than kTopkCap records tie on the selected prefix: finish on the host
-        const size_t total = e->syms.size() * (size_t)e->P;
-        std::vector<bt_summary> all(total);
-        HIPCHK(hipMemcpy(all.data(), e->d_sum[e->cur].p, total * sizeof(bt_summary), hipMemcpyDeviceToHost));
-        res.reserve(total);
-        for (size_t i = 0; i < total; ++i) {
-            const int32_t s = (int32_t)(i / e->P), p = (int32_t)(i % e->P);
-            res.push_back(bt_topk_rec{all[i].sharpe, e->syms[s].id, p, all[i].pnl});
-        }
-        const size_t m = std::min<size_t>(res.size(), (size_t)e->cfg.topk);
-        std::partial_sort(res.begin(), res.begin() + m, res.end(), topk_less);
-        res.resize(m);
-    }
+    // the device selection is complete whatever the ties (k_topk.hip topk_finish_ties)
+    if (n < 0 || n > e->cfg.topk) throw HipFail{"device top-k returned a bad record count"};
+    std::vector<bt_topk_rec> res(e->h_top + 1, e->h_top + 1 + n);
     if ((int32_t)res.size() > k) res.resize(k);
     return res;
 }
@@ -617,11 +604,17 @@ void run_batch_impl(bt_engine* e, size_t n, const bt_job_in* jobs, bt_job_out* o
         }
     });
     int64_t rows = 0;
-    for (JobSlot& j : js)
+    for (size_t i = 0; i < n; ++i) {
+        JobSlot& j = js[i];
+        // what ingest touches: a CSV is parsed whole; a binary payload's header and its four price
+        // columns are validated, its volume column is never read
+        if (j.ok) pr.payload_bytes_read += j.binary ? (int64_t)binary_payload_size(j.bars, false)
+                                                    : (int64_t)jobs[i].len;
         if (j.ok) {
             j.row = rows;
             rows += align_rows(j.bars);
         }
+    }
     const int ncol = hl ? 3 : 1;
     for (int k = 0; k < ncol; ++k) ensure_pinned(e->h_stage[k], e->stage_rows[k], (size_t)std::max<int64_t>(rows, 1));
     parallel_for(nt, n, [&](size_t i) {
@@ -1045,9 +1038,7 @@ int32_t bt_topk_fetch_wait(bt_engine* e, int32_t slot, bt_topk_rec* out, int32_t
         const bt_topk_rec* h = e->h_slot[slot];
         int32_t n = 0;
         memcpy(&n, h, sizeof n);
-        if (n < 0)
-            throw HipFail{"device top-k overflow (more than 2048 ties on the selected prefix): "
-                          "re-run and read with bt_read_topk"};
+        if (n < 0 || n > e->cfg.topk) throw HipFail{"device top-k returned a bad record count"};
         const int32_t m = std::min(n, std::min(k, e->cfg.topk));
         std::copy(h + 1, h + 1 + m, out);
         if (n_trades) {

@@ -506,7 +506,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     if (SEG) {
         if (active) seg_write(a, start_pos, start_e, mine);
         if (helperB && lane < nsp) {
-            ema_mine[lane] = ema_start;
+            // the start record is written by the speculative pass only: a fix pass must leave it
+            // alone, because the other blockIdx.y blocks of this symbol compare it with the
+            // previous segment's end (chain_differs) and may not have done so yet
+            if (fix_seg == 0) ema_mine[lane] = ema_start;
             ema_mine[64 + lane] = ema;  // after the segment's last bar
         }
         return;

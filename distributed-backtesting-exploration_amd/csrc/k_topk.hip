@@ -7,8 +7,10 @@
 //      (key desc, sym asc, param asc) and writes the k result records.
 // Seven small launches, no host round trip; the host reads the count and k records in one copy. The order
 // is exact and deterministic (atomics only decide collection order, which the sort removes).
-// If more than kCap records tie on the 24-bit prefix, finish reports overflow (-1) and the
-// host completes the selection from the raw keys.
+// If more than kCap records tie on the 24-bit prefix (a tie-heavy grid), the finish block
+// completes the exact selection on the device itself (topk_finish_ties), so the result never
+// depends on a host fallback: single-GPU reads and the multi-GPU exchange (comm.cpp) get the same
+// k records.
 #include "internal.h"
 
 namespace bt {
@@ -103,32 +105,153 @@ __global__ __launch_bounds__(256) void topk_collect(const uint64_t* __restrict__
     }
 }
 
+// (sym id, param) of record idx, the tie-break order (ascending) as one 64-bit word.
+__device__ __forceinline__ uint64_t sym_param(const SymDesc* __restrict__ syms, int32_t P,
+                                              unsigned long long idx) {
+    // 32-bit division whenever the index fits (a 64-bit one is a long software sequence)
+    const bool small = idx < (1ULL << 32);
+    const int s = small ? (int)((uint32_t)idx / (uint32_t)P) : (int)(idx / (unsigned long long)P);
+    const int p = (int)(idx - (unsigned long long)s * (unsigned long long)P);
+    return ((uint64_t)(uint32_t)syms[s].id << 32) | (uint32_t)p;
+}
+
+// One block of 256 threads over a 4096-bin histogram h counted from the top bin: the bin that
+// holds the need-th record and how many records lie in the bins above it (the last bin and the
+// total when h holds fewer than need). Same owner search as topk_select; `part` is 256 slots of
+// shared scratch. Every thread returns the result.
+__device__ void block_select(const unsigned int* h, unsigned long long need, unsigned long long* part,
+                             int* bin_out, unsigned long long* above_out) {
+    const int t = threadIdx.x;
+    const int top = kBins - 1 - 16 * t;
+    unsigned long long s = 0;
+    for (int j = 0; j < 16; ++j) s += h[top - j];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const unsigned long long v = t >= d ? part[t - d] : 0ULL;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const unsigned long long incl = part[t], excl = incl - s;
+    const bool owner = (excl < need && incl >= need) || (t == 255 && incl < need);
+    __syncthreads();
+    if (owner) {
+        unsigned long long cum = excl;
+        int bin = top - 15;
+        for (int j = 0; j < 16; ++j) {
+            if (cum + h[top - j] >= need) {
+                bin = top - j;
+                break;
+            }
+            cum += h[top - j];
+        }
+        *bin_out = bin;
+        *above_out = cum;
+    }
+    __syncthreads();
+}
+
+// The degenerate case of topk_finish: more than `cap` records share the selected 24-bit key
+// prefix (a tie-heavy grid, e.g. flat prices where every Sharpe is 0). This block finishes the
+// exact selection itself over the whole key array — the remaining 40 key bits by radix select
+// (digits of 12, 12, 12 and 4 bits), then, among the records equal to the selected key, the
+// (sym id, param) tie-break by a radix select on its complement — and gathers the indices of the
+// min(k, n) best records into ix (at most k <= kTopkMax <= cap of them). Slow (a dozen passes of
+// one block over the keys) but bounded, and only tie-heavy grids take it. Returns the count.
+__device__ int topk_finish_ties(const uint64_t* __restrict__ key, int64_t nrec,
+                                const SymDesc* __restrict__ syms, int32_t P, uint64_t prefix,
+                                uint64_t mask, unsigned long long need, int32_t k,
+                                unsigned int* h, uint64_t* ix, unsigned long long* part) {
+    __shared__ int sh_bin;
+    __shared__ unsigned long long sh_above;
+    __shared__ unsigned int sh_n, sh_eq;
+    const int t = threadIdx.x;
+    // 1. the rest of the key: prefix/mask grow to all 64 bits; need = records wanted at that key
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = pass < 3 ? 28 - 12 * pass : 0;
+        const uint64_t dmask = pass < 3 ? (uint64_t)(kBins - 1) : 15ULL;
+        for (int i = t; i < kBins; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        for (int64_t i = t; i < nrec; i += blockDim.x) {
+            const uint64_t kx = key[i];
+            if ((kx & mask) == prefix) atomicAdd(&h[(kx >> shift) & dmask], 1u);
+        }
+        __syncthreads();
+        block_select(h, need, part, &sh_bin, &sh_above);
+        prefix |= (uint64_t)sh_bin << shift;
+        mask |= dmask << shift;
+        need -= sh_above;
+    }
+    // 2. among key == prefix, the `need` smallest (sym id, param): the largest complements
+    uint64_t tpre = 0, tmask = 0;
+    for (int pass = 0; pass < 6; ++pass) {
+        const int shift = pass < 5 ? 52 - 12 * pass : 0;
+        const uint64_t dmask = pass < 5 ? (uint64_t)(kBins - 1) : 15ULL;
+        for (int i = t; i < kBins; i += blockDim.x) h[i] = 0;
+        __syncthreads();
+        for (int64_t i = t; i < nrec; i += blockDim.x) {
+            if (key[i] != prefix) continue;
+            const uint64_t c = ~sym_param(syms, P, (unsigned long long)i);
+            if ((c & tmask) == tpre) atomicAdd(&h[(c >> shift) & dmask], 1u);
+        }
+        __syncthreads();
+        block_select(h, need, part, &sh_bin, &sh_above);
+        tpre |= (uint64_t)sh_bin << shift;
+        tmask |= dmask << shift;
+        need -= sh_above;
+    }
+    // 3. gather: every key above the selected one, the tied keys whose tie-break ranks above
+    // the selected (sym id, param), and `need` records equal to both (more than one only when
+    // the caller's symbol ids repeat)
+    if (t == 0) {
+        sh_n = 0;
+        sh_eq = 0;
+    }
+    __syncthreads();
+    for (int64_t i = t; i < nrec; i += blockDim.x) {
+        const uint64_t kx = key[i];
+        bool take = kx > prefix;
+        if (kx == prefix) {
+            const uint64_t c = ~sym_param(syms, P, (unsigned long long)i);
+            take = c > tpre || (c == tpre && atomicAdd(&sh_eq, 1u) < need);
+        }
+        if (take) {
+            const unsigned int j = atomicAdd(&sh_n, 1u);
+            if ((int)j < k) ix[j] = (uint64_t)i;
+        }
+    }
+    __syncthreads();
+    const int got = (int)sh_n;
+    return got < k ? got : k;
+}
+
 __global__ __launch_bounds__(256) void topk_finish(
     const uint64_t* __restrict__ key, const bt_summary* __restrict__ sum,
-    const SymDesc* __restrict__ syms, int32_t P, const unsigned int* __restrict__ counts,
+    const SymDesc* __restrict__ syms, int64_t nrec, int32_t P,
+    const unsigned long long* __restrict__ state, const unsigned int* __restrict__ counts,
     const unsigned long long* __restrict__ above, const unsigned long long* __restrict__ cand,
     int cap, int32_t k, bt_topk_rec* __restrict__ out, int32_t* __restrict__ out_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ unsigned long long part[256];
     uint64_t* kk = reinterpret_cast<uint64_t*>(smem);  // order key (desc)
     uint64_t* ss = kk + cap;                            // (sym id, param) (asc)
     uint64_t* ix = ss + cap;                            // record index (payload)
     const int n_above = (int)counts[0], n_cand = (int)counts[1];
-    const int n = n_above + n_cand;
-    if (n > cap) {
-        if (threadIdx.x == 0) out_n[0] = -1;
-        return;
+    int n = n_above + n_cand;
+    const bool ties = n > cap;
+    if (ties) {  // the histogram (16 KB) borrows the key slots, filled only after the gather
+        // state[2]: records still wanted from the prefix group (k minus those above it)
+        n = topk_finish_ties(key, nrec, syms, P, state[0], state[1], state[2], k,
+                             reinterpret_cast<unsigned int*>(kk), ix, part);
     }
     int m = 1;
     while (m < n) m <<= 1;
     for (int i = threadIdx.x; i < m; i += blockDim.x) {
         if (i < n) {
-            const unsigned long long idx = i < n_above ? above[i] : cand[i - n_above];
-            // 32-bit division whenever the index fits (a 64-bit one is a long software sequence)
-            const bool small = idx < (1ULL << 32);
-            const int s = small ? (int)((uint32_t)idx / (uint32_t)P) : (int)(idx / (unsigned long long)P);
-            const int p = (int)(idx - (unsigned long long)s * (unsigned long long)P);
+            const unsigned long long idx = ties ? ix[i] : (i < n_above ? above[i] : cand[i - n_above]);
             kk[i] = key[idx];
-            ss[i] = ((uint64_t)(uint32_t)syms[s].id << 32) | (uint32_t)p;
+            ss[i] = sym_param(syms, P, idx);
             ix[i] = idx;
         } else {  // padding sorts last
             kk[i] = 0;
@@ -210,7 +333,8 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
     // one small block (256 threads, the sort's 2,048 slots in 48 KB of LDS): it finds room on a CU
     // beside the next step's strategy kernel sooner than a 1,024-thread block
     hipLaunchKernelGGL(topk_finish, dim3(1), dim3(256), (size_t)w.cap * 24, st, key, sum, syms,
-                       P, w.counts, w.above, w.cand, w.cap, k, w.out, w.out_n);
+                       n, P, (const unsigned long long*)w.state, w.counts, w.above, w.cand, w.cap,
+                       k, w.out, w.out_n);
     hipLaunchKernelGGL(topk_reset, dim3(1), dim3(64), 0, st, w.state, w.counts);
     return hipGetLastError();
 }

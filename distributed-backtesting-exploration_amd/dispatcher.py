@@ -92,6 +92,7 @@ class Dispatcher:
         self.inflight: Dict[str, tuple] = {}   # id -> (peer, path) until completed
         self.done_paths: Dict[str, str] = {}   # path -> id of its first completion
         self.requeued = 0
+        self.oversize_skips = 0  # replies that could not carry their first file (receive limit)
         self.failed_paths: List[str] = []     # unreadable / undeliverable (counted done)
         self.done_lock = threading.Lock()
         self.results_path = results_path
@@ -159,6 +160,10 @@ class Dispatcher:
             peer = self.peers.get(ctx.peer())
             if peer is not None:
                 peer["status"] = req.status
+                # a status from a known peer is a sign of life as well (the reference refreshes
+                # only on RequestJobs, main.rs:105-113): a worker connection that is throttled
+                # and only keeps alive must not be pruned with jobs it still holds
+                peer["last_connection"] = time.time()
         return P.StatusReply()
 
     def _reply_cap(self, ctx) -> int:
@@ -204,13 +209,18 @@ class Dispatcher:
                 self._drop_unreadable(path)
                 continue
             need = len(data) + JOB_OVERHEAD
+            if need > self.max_reply_bytes:  # no worker can ever receive it from this server
+                log.error("%s (%d bytes) exceeds the server's send limit", path, len(data))
+                self._drop_unreadable(path)
+                continue
             if size + need > cap:
-                if not jobs and need > cap:  # can never be delivered to this worker
-                    log.error("%s (%d bytes) exceeds the worker's receive limit", path, len(data))
-                    self._drop_unreadable(path)
-                    continue
+                # too large for what is left of this reply, or for this worker's receive limit
+                # altogether: back to the queue, for a later request or a worker with a larger
+                # limit (--max-receive-mb) to take
                 with self.files_lock:
                     self.files.extend(files[i:])
+                    if not jobs and need > cap:
+                        self.oversize_skips += 1
                 break
             size += need
             with self.done_lock:

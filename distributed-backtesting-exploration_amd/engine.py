@@ -72,7 +72,8 @@ class _JobOut(C.Structure):
 
 class _BatchProfile(C.Structure):
     _fields_ = [("n_jobs", C.c_int64), ("n_failed", C.c_int64), ("payload_bytes", C.c_int64),
-                ("bars", C.c_int64), ("host_ingest_ms", C.c_double), ("upload_ms", C.c_double),
+                ("payload_bytes_read", C.c_int64), ("bars", C.c_int64),
+                ("host_ingest_ms", C.c_double), ("upload_ms", C.c_double),
                 ("compute_ms", C.c_double), ("readback_ms", C.c_double),
                 ("format_ms", C.c_double), ("total_ms", C.c_double)]
 

@@ -106,6 +106,9 @@ class Worker:
         self.max_queued_bytes = max_queued_bytes or max(4 * max_batch_bytes, 1 << 30)
         self._queued = 0
         self._qlock = threading.Lock()
+        # completions whose CompleteJob failed: (id, data, retry time, attempts)
+        self._retry: list = []
+        self.retry_base_s, self.retry_max_s = 0.25, 8.0
         self._opts = [("grpc.max_receive_message_length", max_receive)]
         self.channel = grpc.insecure_channel(target, options=self._opts)
         u = self.channel.unary_unary
@@ -132,13 +135,23 @@ class Worker:
         """Extra fetcher `idx` >= 1: RequestJobs on its own connection while the queue has room."""
         ch = grpc.insecure_channel(self.target, options=self._opts + [
             ("grpc.use_local_subchannel_pool", 1), ("dbx.fetcher", idx)])
-        req = ch.unary_unary(P.method_path("RequestJobs"), request_serializer=lambda m: m.SerializeToString(),
+        ser = lambda m: m.SerializeToString()  # noqa: E731
+        req = ch.unary_unary(P.method_path("RequestJobs"), request_serializer=ser,
                              response_deserializer=P.JobsReply.FromString)
+        status = ch.unary_unary(P.method_path("SendStatus"), request_serializer=ser,
+                                response_deserializer=P.StatusReply.FromString)
         try:
             while not self.stop.is_set():
                 with self._qlock:
                     full = self._queued >= self.max_queued_bytes
                 if full:
+                    # a keep-alive on this connection while throttled: the dispatcher keys peers
+                    # by connection, and one silent for its prune window would have the jobs it
+                    # still holds in this worker's queue re-dispatched (duplicate GPU work)
+                    try:
+                        status(P.StatusRequest(status=P.RUNNING))
+                    except grpc.RpcError:
+                        pass
                     time.sleep(self.job_tick)
                     continue
                 try:
@@ -218,22 +231,37 @@ class Worker:
                     next_job = now + self.job_tick
                 # main.rs:80-83: a completion is sent as soon as it is ready (the select loop
                 # takes ready completions between ticks), so every queued one goes now
-                try:
-                    jid, data = self.complete_q.get(timeout=0.01)
-                    while True:
-                        try:
-                            self._complete(P.CompleteRequest(id=jid, data=data))
-                        except grpc.RpcError as why:  # the reference unwraps (panics) here
-                            log.error("Unable to complete %s: %s", jid, why)
-                        jid, data = self.complete_q.get_nowait()
-                except queue.Empty:
-                    pass
+                self._send_completions()
         finally:
             self.stop.set()
             th.join(timeout=5)
             for f in fetch:
                 f.join(timeout=5)
             self.channel.close()
+
+    def _send_completions(self):
+        """Send every ready completion. One that fails (the reference unwraps and panics here,
+        main.rs:80-83, which ends the worker so the server prunes it and its jobs are lost) is
+        kept and retried with a capped exponential backoff: the dispatcher keeps the job in
+        flight until its completion arrives, so dropping it would leave the run unfinished."""
+        now = time.monotonic()
+        due = [r for r in self._retry if r[2] <= now]
+        self._retry = [r for r in self._retry if r[2] > now]
+        try:
+            if not due:
+                due.append(self.complete_q.get(timeout=0.01) + (now, 0))
+            while True:
+                while due:
+                    jid, data, _, tries = due.pop(0)
+                    try:
+                        self._complete(P.CompleteRequest(id=jid, data=data))
+                    except grpc.RpcError as why:
+                        log.error("Unable to complete %s (attempt %d): %s", jid, tries + 1, why)
+                        back = min(self.retry_max_s, self.retry_base_s * (2 ** tries))
+                        self._retry.append((jid, data, time.monotonic() + back, tries + 1))
+                due.append(self.complete_q.get_nowait() + (now, 0))
+        except queue.Empty:
+            pass
 
 
 def main(argv=None):

@@ -25,7 +25,10 @@
 extern "C" {
 #endif
 
-#define BT_ABI_VERSION 1
+/* 2: bt_batch_profile.payload_bytes_read; the device top-k never overflows (bt_topk_fetch_wait
+ *    and bt_exchange_wait return exact records on tie-heavy grids); bt_summary.hash is the
+ *    additive trade hash of docs/oracle_spec.md §4 (version 1 hosts may hold FNV-1a hashes). */
+#define BT_ABI_VERSION 2
 
 typedef struct bt_engine bt_engine;
 
@@ -147,6 +150,9 @@ int32_t bt_last_segments(bt_engine* e, int64_t* refixed_blocks);
 typedef struct bt_batch_profile {
     int64_t n_jobs, n_failed;
     int64_t payload_bytes;            /* sum of Job.File lengths */
+    int64_t payload_bytes_read;       /* bytes ingest actually reads: a CSV whole, a DBXCOL1
+                                         payload its header and price columns (never the
+                                         volume column) */
     int64_t bars;                     /* bars of the good jobs */
     double host_ingest_ms;            /* parse / validate + copy into pinned staging */
     double upload_ms;                 /* H2D of the staged columns */
@@ -182,9 +188,9 @@ int32_t bt_read_stats(bt_engine* e, bt_stats* out);
 /* Pipelined read-back of the last run's top-k and trade count: bt_topk_fetch_async enqueues
  * the device-to-host copy into pinned slot 0 or 1 behind the run (no host wait), so the next
  * bt_run can be enqueued before this run's records are consumed; bt_topk_fetch_wait waits for
- * that copy only and returns the record count (or -1 if the device selection overflowed — more
- * than 2,048 records tie on the selected key prefix — in which case re-run and use
- * bt_read_topk, which finishes on the host). A slot stays valid until its next fetch. */
+ * that copy only and returns the record count. The device selection is exact on any grid (a
+ * tie-heavy one takes a slower single-block finish, k_topk.hip). A slot stays valid until its
+ * next fetch. */
 int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot);
 int32_t bt_topk_fetch_wait(bt_engine* e, int32_t slot, bt_topk_rec* out, int32_t k,
                            int64_t* n_trades);

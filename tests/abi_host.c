@@ -34,7 +34,8 @@ static int layout(void) {
     SZ(bt_summary); OFF(bt_summary, pnl); OFF(bt_summary, sharpe); OFF(bt_summary, hash);
     SZ(bt_trade); OFF(bt_trade, entry_px);
     SZ(bt_sums); SZ(bt_topk_rec); OFF(bt_topk_rec, sym); OFF(bt_topk_rec, pnl);
-    SZ(bt_stats); SZ(bt_batch_profile); OFF(bt_batch_profile, host_ingest_ms);
+    SZ(bt_stats); SZ(bt_batch_profile); OFF(bt_batch_profile, payload_bytes_read);
+    OFF(bt_batch_profile, bars); OFF(bt_batch_profile, host_ingest_ms);
     OFF(bt_batch_profile, total_ms);
     printf("\"abi_version\": %d}\n", (int)bt_abi_version());
     return 0;

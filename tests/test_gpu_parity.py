@@ -175,17 +175,62 @@ def test_config2_full_shape_sampled_parity():
     assert [(int(t["sym"]), int(t["param"])) for t in top] == exp
 
 
-def test_topk_massive_ties_host_finish():
-    """More records tie on the selected key prefix than the device finish can sort: every
-    Sharpe is 0 on flat prices, so the order is (sym asc, param asc) — the host path."""
+def _expected_topk(allr, sym_ids, k):
+    P = allr.shape[1]
+    flat = allr.reshape(-1)
+    ids = np.repeat(np.asarray(sym_ids, np.int64), P)
+    order = np.lexsort((np.tile(np.arange(P), len(sym_ids)), ids, -flat["sharpe"]))
+    return [(int(ids[i]), int(i % P)) for i in order[:k]]
+
+
+def test_topk_massive_ties_device_finish():
+    """More records tie on the selected key prefix than the finish block's sort holds: every
+    Sharpe is 0 on flat prices, so the order is (sym asc, param asc). The device completes the
+    selection itself (k_topk.hip topk_finish_ties): the synchronous read, the pipelined fetch and
+    the C-ABI RCCL exchange (world 1) all return the same 50 records."""
     grid = D.Grid.sma([2, 3, 4], [5, 6, 7], annualization=252)
     closes = [np.full(200, 1_000_000, np.int32) for _ in range(300)]   # 2,700 records
-    with D.Engine(grid, topk=50) as e:
-        e.load_ohlc(closes, sym_ids=np.arange(1000, 1300))
+    exp = [(1000 + i // 9, i % 9) for i in range(50)]
+    comm = E.Comm(E.Comm.unique_id(), 0, 1, 0, 50)
+    try:
+        with D.Engine(grid, topk=50) as e:
+            e.load_ohlc(closes, sym_ids=np.arange(1000, 1300))
+            e.run()
+            top = e.read_topk()
+            e.topk_fetch_async(0)
+            fetched, trades = e.topk_fetch_wait(0)
+            comm.exchange_async(e, 1)
+            gathered, cnt = comm.exchange_wait(1)
+    finally:
+        comm.close()
+    for recs in (top, fetched, gathered):
+        assert [(int(t["sym"]), int(t["param"])) for t in recs] == exp
+        assert all(float(t["sharpe"]) == 0.0 for t in recs)
+    assert trades == 0 and cnt == [300 * 200 * 9, 0]
+
+
+@pytest.mark.parametrize("k", [1, 50, 1024])
+def test_topk_ties_mixed_with_winners(k):
+    """Tie-heavy grid with real winners and losers around the tied value, symbol ids not in
+    index order: records above the tied Sharpe come first, then the ties by (sym id, param);
+    up to the largest k the engine accepts."""
+    grid = D.Grid.sma([2, 3, 4, 5], [8, 9, 11], annualization=252)
+    rng = np.random.default_rng(7)
+    closes = []
+    for s in range(900):
+        if s % 30 == 0:  # a trending or noisy series: non-zero Sharpes on both sides of 0
+            c = np.clip(1_000_000 + np.cumsum(rng.integers(-4000, 4400, 400)), 10_000, 2**31 - 1)
+            closes.append(c.astype(np.int32))
+        else:
+            closes.append(np.full(400, 2_000_000, np.int32))
+    ids = rng.permutation(np.arange(5000, 5900))
+    with D.Engine(grid, topk=k) as e:
+        e.load_ohlc(closes, sym_ids=ids)
         e.run()
+        allr = e.summaries().copy()
         top = e.read_topk()
-    assert [(int(t["sym"]), int(t["param"])) for t in top] == [(1000 + i // 9, i % 9) for i in range(50)]
-    assert all(float(t["sharpe"]) == 0.0 for t in top)
+    assert (allr["sharpe"] == 0).sum() > 2048  # the tie path really runs
+    assert [(int(t["sym"]), int(t["param"])) for t in top] == _expected_topk(allr, ids, k)
 
 
 TILE_GRIDS = {
@@ -446,6 +491,10 @@ def test_run_batch_binary_and_csv_mixed():
         st = e.stats()
     assert prof["n_jobs"] == 6 and prof["n_failed"] == 3 and st["errors"] == 3
     assert prof["bars"] == 9000 and prof["payload_bytes"] == sum(len(b) for _, b in jobs)
+    # bytes ingest reads: job 0's volume column is skipped; job 1 fails its header check unread;
+    # jobs 3 and 5 are read whole before their validation fails
+    assert prof["payload_bytes_read"] == (16 + 16 * len(o[0])) + len(good[2]) + len(good[4]) \
+        + len(bad[3]) + len(bad[5])
     for i, b in bad.items():
         assert res[i][0] < 0
         with pytest.raises(ValueError) as why:

@@ -135,6 +135,28 @@ def test_ema_split_ragged_and_empty_segments():
             compare_summary(ref[i, p], orc[p], f"ema ragged {lengths[i]} bars {grid.param(p)}")
 
 
+@pytest.mark.parametrize("segments,burn", [(3, 1), (2, 2)])
+def test_ema_split_many_param_blocks(segments, burn):
+    """EMA+OLS grid of more than 896 params (64 lanes x 14 parameter waves), so each symbol's
+    parameters span several blockIdx.y blocks that share the per-(segment, symbol) chain record:
+    with a burn-in too short for the chains to meet, the fix pass must re-walk every y-block of
+    a boundary (a fix pass that rewrote the shared start record would let later y-blocks keep
+    results built on the wrong chain)."""
+    spans = list(range(3, 3 + 2 * 30, 2))          # 30 spans
+    wins = list(range(4, 4 + 5 * 32, 5))           # 32 OLS windows -> 960 params
+    grid = D.Grid.ema_ols(spans, wins, band_bps=15)
+    assert grid.n_params > 896
+    cols = [F.gen(0x5EED, 400 + i, 12000 + 3000 * i, 1) for i in range(3)]
+    ref, used1, _ = _run_grid(grid, cols, 1)
+    got, used, refixed = _run_grid(grid, cols, segments, burn)
+    assert used1 == 1 and used == segments and refixed > 0
+    assert got.tobytes() == ref.tobytes(), "split run differs from the unsplit run"
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("ema_ols", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(0, grid.n_params, 7):
+            compare_summary(got[i, p], orc[p], f"ema y-blocks G={segments} sym {i} {grid.param(p)}")
+
+
 def test_ema_auto_split_config3_grid_small_shard():
     """Config-3 grid on a small shard (automatic split) against the oracle on sampled symbols."""
     grid = D.config3_grid()

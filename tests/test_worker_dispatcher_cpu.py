@@ -123,22 +123,73 @@ def test_reply_capped_below_worker_receive_limit(tmp_path):
 
 
 def test_unreadable_and_undeliverable_paths_count_as_finished(tmp_path):
+    """An unreadable path, or one larger than the server's own send limit, is finished (failed);
+    one that is only larger than the asking worker's receive limit stays queued for a worker
+    with a larger limit (--max-receive-mb)."""
     good = tmp_path / "good"
     good.write_bytes(b"2020-01-01,1,1,1,1,1\n")
     big = tmp_path / "big"
     big.write_bytes(b"y" * 5000)
-    paths = [str(tmp_path / "missing"), str(good), str(big)]
-    d = DSP.Dispatcher(paths)
+    huge = tmp_path / "huge"
+    huge.write_bytes(b"z" * 20000)
+    paths = [str(tmp_path / "missing"), str(huge), str(good), str(big)]
+    d = DSP.Dispatcher(paths, max_reply_bytes=10000)
     try:
         md = ((P.MAX_RECEIVE_KEY, str(DSP.REPLY_MARGIN + 1000)),)
         r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))
         assert [d.job_paths[j.id] for j in r.jobs] == [str(good)]
-        assert d.failed_paths == [str(tmp_path / "missing")] and d.files == [str(big)]
-        r2 = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))   # big alone cannot fit
-        assert len(r2.jobs) == 0 and not d.files
-        assert sorted(d.failed_paths) == sorted([str(tmp_path / "missing"), str(big)])
-        assert not d.all_done()
+        assert sorted(d.failed_paths) == sorted([str(tmp_path / "missing"), str(huge)])
+        assert d.files == [str(big)]
+        r2 = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))   # big cannot reach "a"...
+        assert len(r2.jobs) == 0 and d.files == [str(big)] and d.oversize_skips == 1
         d.complete_job(P.CompleteRequest(id=r.jobs[0].id, data="ok"), _Ctx("a"))
+        assert not d.all_done()
+        r3 = d.request_jobs(P.JobsRequest(cores=0), _Ctx("b"))        # ...but reaches "b"
+        assert [d.job_paths[j.id] for j in r3.jobs] == [str(big)] and not d.files
+        d.complete_job(P.CompleteRequest(id=r3.jobs[0].id, data="ok"), _Ctx("b"))
         assert d.all_done()                                           # --exit-when-done ends
+    finally:
+        d.close()
+
+
+def test_failed_complete_job_is_retried_until_the_dispatcher_is_done(tmp_path):
+    """A CompleteJob RPC that fails is kept and retried with backoff (dropping it would leave
+    the job in flight forever and --exit-when-done would never end)."""
+    import grpc
+    p = tmp_path / "f0"
+    p.write_bytes(b"2020-01-01,1,1,1,1,1\n")
+    d = DSP.Dispatcher([str(p)])
+    calls = {"n": 0}
+
+    def flaky(req):
+        calls["n"] += 1
+        if calls["n"] == 1:
+            raise grpc.RpcError("transient")
+        return d.complete_job(req, _Ctx("w"))
+    w = WK.Worker("127.0.0.1:1", lambda jobs: ["ok"] * len(jobs), cores=1)
+    w.retry_base_s = 0.02
+    w._complete = flaky
+    try:
+        r = d.request_jobs(P.JobsRequest(cores=1), _Ctx("w"))
+        WK.process_incoming_job(r, w.complete_q, w.processor)
+        t0 = time.time()
+        while not d.all_done() and time.time() - t0 < 5:
+            w._send_completions()
+        assert d.all_done() and calls["n"] == 2 and not w._retry
+    finally:
+        w.channel.close()
+        d.close()
+
+
+def test_status_keeps_a_peer_alive():
+    """SendStatus from a known peer refreshes its last connection (a throttled fetcher's
+    keep-alive), so the health thread does not prune it and re-dispatch its jobs."""
+    d = DSP.Dispatcher([], prune_after_s=3600)
+    try:
+        d.peers["w"] = {"status": P.IDLE, "last_connection": 0.0}
+        d.send_status(P.StatusRequest(status=P.RUNNING), _Ctx("w"))
+        assert time.time() - d.peers["w"]["last_connection"] < 5
+        d.send_status(P.StatusRequest(status=P.RUNNING), _Ctx("stranger"))
+        assert "stranger" not in d.peers                 # main.rs:80-102: no upsert on status
     finally:
         d.close()
