@@ -219,7 +219,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
                 e->grid.kn2[q] = (double)(kn * kn);  // exact: kn <= 2^20
             }
             e->grid.kmin_idx = (int32_t)(std::min_element(e->ax[1].begin(), e->ax[1].end()) - e->ax[1].begin());
-            if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
+            if (boll_lds_bytes(e->grid, 1) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;
         }
         default:
@@ -375,9 +375,26 @@ void run_impl(bt_engine* e) {
     }
     hipError_t err = hipSuccess;
     switch (e->cfg.strategy) {
-        case BT_SMA_CROSS:
-            err = launch_sma(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, e->stream);
+        case BT_SMA_CROSS: {
+            // bar segments (k_sma.hip) for shards of few, long one-block-per-CU symbols
+            SegArgs sg{nullptr, nullptr, nullptr, 1, e->seg_burn_set ? e->seg_burn : kSmaBurnTiles};
+            if (!parity) {
+                int32_t maxb = 0;
+                for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);
+                sg.G = e->seg_req > 0 ? e->seg_req
+                                      : sma_auto_segments(S, e->P, maxb, e->grid.wmax, sg.burn_tiles);
+            }
+            if (sg.G > 1) {
+                e->d_seg.ensure(2 * (size_t)sg.G * S * e->P);  // SmaSegRec: two SegRec slots
+                e->d_refixed.ensure(1);
+                HIPCHK(hipMemsetAsync(e->d_refixed.p, 0, sizeof(unsigned long long), e->stream));
+                sg.rec = e->d_seg.p;
+                sg.refixed = e->d_refixed.p;
+            }
+            e->seg_last = sg.G;
+            err = launch_sma(e->d_syms.p, S, e->d_c.p, e->grid, out, parity, sg, e->stream);
             break;
+        }
         case BT_EMA_OLS: {
             int32_t maxspan = 1, maxb = 0;
             for (int32_t v : e->ax[0]) maxspan = std::max(maxspan, v);

@@ -82,6 +82,29 @@ struct SegRec {
     int64_t s2hi;
 };
 static_assert(sizeof(SegRec) == 128, "SegRec layout");
+// SMA bar segments (k_sma.hip): an SMA position is held from one crossover to the next, often
+// for thousands of bars, so a segment cannot burn in to the entry of the trade open at its start.
+// That trade is carried symbolically: the segment records where and at what price it closes
+// and its path from the segment start, and the combine pass, which knows the entry from the
+// earlier segments, closes it. Occupies two SegRec slots per (segment, symbol, param).
+struct SmaSegRec {
+    int32_t ntr;                   // trades closed in the segment (the carried one included)
+    int32_t e0;                    // first entry from flat in the segment (-1: none)
+    int32_t start_pos, end_pos;    // position entering the first accounted bar / after the last
+    int32_t end_e, end_ce;         // trade open at the end, opened in the segment (end_e = -1:
+                                   // the carried trade is still open: entry unknown here)
+    int32_t x1, px1;               // the carried trade's exit bar (-1: still open) and fill
+    int32_t agg1[4];               // its path from the segment start to x1 (or to the end)
+    int32_t end_agg[4];            // path of the trade open at the end, from its entry
+    int64_t R;                     // pnl of the other trades closed in the segment
+    int64_t A, B, C, D;            // their drawdown forms (SegRec)
+    uint64_t h;                    // their additive hash
+    uint64_t s1lo;
+    int64_t s1hi;
+    uint64_t s2lo;
+    int64_t s2hi;
+};
+static_assert(sizeof(SmaSegRec) <= 2 * sizeof(SegRec), "SmaSegRec fits two SegRec slots");
 struct SegArgs {
     SegRec* rec;
     unsigned long long* refixed;   // fix-pass blocks that re-walked their segment
@@ -103,9 +126,15 @@ struct SmaShape {                     // SMA launch shape for P parameters (k_sm
 };
 SmaShape sma_shape(int P);
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                      const Out& out, bool parity, hipStream_t st);
+                      const Out& out, bool parity, const SegArgs& seg, hipStream_t st);
+// SMA segments for this shard (auto mode) and the default burn-in (k_sma.hip)
+int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int32_t wmax,
+                          int32_t burn_tiles);
+constexpr int kSmaBurnTiles = 2;
+int device_cus();  // compute units of the current device
 size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
-size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
+// dynamic LDS of the Bollinger tile kernel with nsplit finder/accountant pairs (1 or 2)
+size_t boll_lds_bytes(const Grid& g, int nsplit = 2);
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, const SegArgs& seg, hipStream_t st);
 // EMA+OLS segments: count for this shard (auto mode) and the burn-in a speculative segment needs

@@ -23,9 +23,10 @@
 //            ~L + G + [pos == +1]). Each lane walks only its flips (ctz): per trade O(1) work —
 //            PnL, MTM drawdown from the DST, Sharpe sums as int128 prefix differences, hash.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
-#include "device_common.h"
+#include "tile_common.h"
 
 namespace bt {
 
@@ -210,6 +211,13 @@ struct SmaAcct {
     uint64_t ps1, ps2, h;
     i128 s1, s2;
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
+    // bar segments (SEG) only: the drawdown as max-plus forms of the unknown entering gap and mdd
+    // (tile_common.h TradeAcct), and the trade open at the segment start, whose entry lies in an
+    // earlier segment: `carried` while it is open, then its exit bar x1, fill px1 and path agg1
+    // from the segment start (closed by the combine pass, internal.h SmaSegRec)
+    int64_t A, Bq, C, D;
+    int32_t carried, x1, px1;
+    Agg agg1;
 };
 
 // SMA positions: flat until the first decision, then every flip reverses (fast > slow is
@@ -218,17 +226,35 @@ struct SmaAcct {
 
 // Closes the open trade at in-tile bar b (fill cx = close of bar t = t0 + b).
 // MERGE = false: the trade opened in this tile (a.agg is the identity), so seg is its whole path.
-template <bool PARITY, bool MERGE = true>
+// SEG: a close of the carried trade (only possible with MERGE: the first close of a tile) is
+// recorded for the combine pass instead of accounted.
+template <bool PARITY, bool MERGE = true, bool SEG = false>
 __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int32_t cx,
                                           bt_trade* tr, int cap) {
     const Agg st = MERGE ? agg_merge(a.agg, seg) : seg;   // seg: closes [sb, b] of this tile
+    if (SEG && MERGE && a.carried) {
+        a.x1 = t;
+        a.px1 = cx;
+        a.agg1 = st;
+        a.carried = 0;
+        a.ntr++;
+        return;
+    }
     const bool lg = a.pos > 0;
     const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;   // |.| < 2^31
     const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
     const int32_t path = lg ? st.dd : st.du;
     const int32_t pnl = lg ? cx - a.ce : a.ce - cx;
-    a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
-    a.gap = max(a.gap, (int64_t)hi) - pnl;
+    if (SEG) {
+        const int64_t A0 = a.A, B0 = a.Bq;
+        a.C = max(a.C, A0 - (int64_t)lo);
+        a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
+        a.A = A0 - pnl;
+        a.Bq = max(B0, (int64_t)hi) - pnl;
+    } else {
+        a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+        a.gap = max(a.gap, (int64_t)hi) - pnl;
+    }
     a.R += pnl;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)lg << 62);
@@ -259,7 +285,7 @@ __device__ __forceinline__ void sma_open(SmaAcct& a, int b, int t, int32_t cx, i
 // closing trade may carry a path from earlier tiles (a.agg); every later reversal of the tile
 // closes a trade opened at the previous flip, so it skips the merge and leaves a.agg alone
 // (already the identity).
-template <bool PARITY, bool ONE_TRIP, bool FIRST>
+template <bool PARITY, bool ONE_TRIP, bool FIRST, bool SEG>
 __device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& alt, int t0,
                                             const int32_t* cT, const int64_t* ql, const Agg* D,
                                             bt_trade* tr, int cap) {
@@ -287,14 +313,14 @@ __device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& a
         qb = (uint64_t)ql[b];
     }
     alt = qb - alt;
-    sma_close<PARITY, FIRST>(a, seg, t0 + b, cx, tr, cap);
+    sma_close<PARITY, FIRST, SEG>(a, seg, t0 + b, cx, tr, cap);
     sma_open<FIRST>(a, b, t0 + b, cx, -a.pos);
 }
 
 // The tile's flips F (bar order). Sharpe partials: a close adds +pos * QL[b], an open subtracts
 // np * QL[b] (a reversal adds 2 pos QL[b]); the squared sum changes only on the first entry
 // (-Q2L[b]) and the forced exit (+Q2L[b]).
-template <bool PARITY, bool ONE_TRIP>
+template <bool PARITY, bool ONE_TRIP, bool SEG>
 __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl, uint64_t LONG,
                                           const int32_t* cT, const int64_t* ql, const Agg* D,
                                           bt_trade* tr, int cap) {
@@ -314,23 +340,31 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     // p_k = (-1)^(k-1) p_1 and adds 2 p_k QL[b_k]: an alternating sum, carried as
     // alt_k = QL[b_k] - alt_(k-1), so that sum = 2 p_n alt_n = -2 pos alt after the loop
     uint64_t alt = 0;
-    if (F) sma_reverse<PARITY, ONE_TRIP, true>(a, F, alt, t0, cT, ql, D, tr, cap);
-    while (F) sma_reverse<PARITY, ONE_TRIP, false>(a, F, alt, t0, cT, ql, D, tr, cap);
+    if (F) sma_reverse<PARITY, ONE_TRIP, true, SEG>(a, F, alt, t0, cT, ql, D, tr, cap);
+    while (F) sma_reverse<PARITY, ONE_TRIP, false, SEG>(a, F, alt, t0, cT, ql, D, tr, cap);
     a.ps1 += a.pos > 0 ? (uint64_t)0 - (alt << 1) : alt << 1;
     if (FX) {  // flat after bar B-1 (only set when a position is open before it)
         const int b = bl;
         const uint64_t qx = (uint64_t)ql[b];
-        sma_close<PARITY>(a, dst_query_bf(D, a.sb, b), t0 + b, cT[b], tr, cap);
+        sma_close<PARITY, true, SEG>(a, dst_query_bf(D, a.sb, b), t0 + b, cT[b], tr, cap);
         a.ps1 += a.pos > 0 ? qx : (uint64_t)0 - qx;
         a.ps2 += (uint64_t)ql[kTile + b];
         a.pos = 0;
     }
 }
 
-template <bool PARITY, bool STAMPS, bool ONE_TRIP>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(const SymDesc* __restrict__ syms,
-                                                   const int32_t* __restrict__ close, Grid g,
-                                                   Out out, int dedicated) {
+// The kernel body. SEG: one bar segment per block (blockIdx.z = segment, or with fix_seg >= 1 the
+// fix pass of that boundary), results into SmaSegRec records (internal.h) that sma_seg_combine
+// folds. A segment s >= 1 scans the ring alone over the windows' lookback (the prefix sums only),
+// walks `burn` tiles before its first bar starting flat (an SMA position is the sign of the last
+// strict crossover comparison, so one decided bar sets it), and carries the trade open at its
+// first bar symbolically (SmaAcct::carried). The fix pass re-walks a segment whose lanes started
+// in a position other than the previous segment's last one (a burn-in of tied comparisons only).
+template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool SEG>
+__device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
+                                         const int32_t* __restrict__ close, const Grid& g,
+                                         const Out& out, int dedicated, const SegArgs& sg,
+                                         int fix_seg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nf = g.na, ns = g.nb, nw = nf + ns;
     const int R = g.ring;
@@ -371,38 +405,76 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     const int p = (kf * ns) + (ks - nf);
     const int32_t* crow = close + sd.off;
 
+    // tiles of this block: ring-only lookback from T_scan, walked from T_walk, accounted from
+    // T_acct, up to T_end (exclusive); all tiles without SEG
+    SegRange sr{0, 0, 0, 0, ntiles};
+    SmaSegRec* mine = nullptr;
+    const SmaSegRec* prev = nullptr;
+    if (SEG) {
+        sr = seg_range(sg, fix_seg, ntiles, g.wmax);
+        const size_t per_seg = (size_t)gridDim.x * P;
+        mine = reinterpret_cast<SmaSegRec*>(sg.rec) + sr.seg * per_seg + (size_t)blockIdx.x * P + p;
+        if (sr.seg > 0) prev = mine - per_seg;
+        if (fix_seg > 0) {  // re-walk only if some lane started in a position other than the true one
+            if (!__syncthreads_or(active && mine->start_pos != prev->end_pos)) return;
+            if (tid == 0) atomicAdd(sg.refixed, 1ULL);
+        }
+    }
+    const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
+
     const int nwp = (nw + kKeyGrab - 1) / kKeyGrab * kKeyGrab;
+    const uint32_t key_round = (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + nwaves);
     for (int w = tid; w < nwp; w += blockDim.x) {
         const int W = w < nf ? g.a[w] : (w < nw ? g.b[w - nf] : 1);
         win[w] = W;
         invw[w] = key_recip(W);
     }
     if (tid == 0) {
-        ring[0] = 0.0;
-        *ctr = 0;
+        ring[(T_scan * kTile) & (R - 1)] = 0.0;  // prefix base: sums over scanned bars
+        *ctr = (uint32_t)T_walk * key_round;     // key rounds are numbered by tile
     }
     __syncthreads();
     const int fw = win[kf], sw = win[ks];
     const int warm = (fw > sw ? fw : sw) - 1;  // first decision bar of this lane
 
-    ScanCarry cy{0, 0};
-    // prologue: stage 1 for tiles 0, 1; stage 2 for tile 0. The helper keeps the closes of the
-    // tile after next in flight (cpre) across the barrier.
+    ScanCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
+    // SEG lookback: the prefix ring over the windows before the first walked bar (the next tile's
+    // closes in flight while one is summed)
+    if (SEG && helper && T_scan < T_walk) {
+        int32_t cn = load_close(crow, B, T_scan * kTile + lane);
+#pragma unroll 1
+        for (int T = T_scan; T < T_walk; ++T) {
+            const int32_t c = cn;
+            cn = load_close(crow, B, (T + 1) * kTile + lane);
+            const int64_t inc = wave_iscan_i64((int64_t)c);
+            ring[(T * kTile + lane + 1) & (R - 1)] = (double)(cy.P + inc);
+            cy.P += lane63_i64(inc);
+            cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
+        }
+    }
+    // prologue: stage 1 for the first two walked tiles; stage 2 for the first. The helper keeps
+    // the closes of the tile after next in flight (cpre) across the barrier.
     int32_t cpre = 0;
     if (helper || dstw) {
-        const int32_t c0 = load_close(crow, B, lane), c1 = load_close(crow, B, kTile + lane);
-        cpre = load_close(crow, B, 2 * kTile + lane);
-        if (helper) stage_ring(c0, B, 0, lane, R, ring, cts, qls, cy);
-        if (dstw || dsth) stage_dst(c0, lane, dst);
+        const int b0 = T_walk * kTile;
+        const int32_t c0 = load_close(crow, B, b0 + lane), c1 = load_close(crow, B, b0 + kTile + lane);
+        cpre = load_close(crow, B, b0 + 2 * kTile + lane);
+        const int s0 = T_walk % kStages, s1 = (T_walk + 1) % kStages;
+        if (T_walk < T_end) {
+            if (helper) stage_ring(c0, B, b0, lane, R, ring, cts + s0 * kTile, qls + s0 * 2 * kTile, cy);
+            if (dstw || dsth) stage_dst(c0, lane, dst + s0 * kDstLevels * kTile);
+        }
         __syncthreads();
-        if (ntiles > 1) {
-            if (helper) stage_ring(c1, B, kTile, lane, R, ring, cts + kTile, qls + 2 * kTile, cy);
-            if (dstw || dsth) stage_dst(c1, lane, dst + kDstLevels * kTile);
+        if (T_walk + 1 < T_end) {
+            if (helper) stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, cy);
+            if (dstw || dsth) stage_dst(c1, lane, dst + s1 * kDstLevels * kTile);
         }
     } else {
         __syncthreads();
     }
-    stage_keys(0, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys, ctr, 0, nwaves, lane);
+    if (T_walk < T_end)
+        stage_keys(T_walk * kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw,
+                   keys + (T_walk & 1) * nwp * kKS, ctr, (uint32_t)T_walk, nwaves, lane);
     __syncthreads();
 
     SmaAcct a;
@@ -412,6 +484,32 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     a.h = 0;
     a.s1 = a.s2 = 0;
     a.agg = kAggId;
+    a.A = 0;
+    a.Bq = a.C = a.D = kNegInf;
+    a.carried = a.x1 = a.px1 = 0;
+    a.agg1 = kAggId;
+    int32_t start_pos = 0;
+    if (SEG && fix_seg > 0 && active) a.pos = prev->end_pos;  // the true position entering
+    // SEG: at the first accounted bar keep the position, drop the burn-in's accounts, and carry
+    // the open trade (its entry lies before the segment) symbolically from here
+    auto enter_acct = [&]() {
+        start_pos = a.pos;
+        a.carried = a.pos != 0;
+        a.agg = kAggId;
+        a.sb = 0;
+        a.R = 0;
+        a.A = 0;
+        a.Bq = a.C = a.D = kNegInf;
+        a.ntr = 0;
+        a.h = 0;
+        a.s1 = a.s2 = 0;
+        a.ps1 = a.ps2 = 0;
+        a.e0 = -1;
+        a.x1 = -1;
+        a.px1 = 0;
+        a.agg1 = kAggId;
+    };
+    if (SEG && T_walk == T_acct) enter_acct();
     bt_trade* tr = nullptr;
     const size_t gi = (size_t)blockIdx.x * P + p;
     if (PARITY && active) tr = out.trades + gi * out.trade_cap;
@@ -429,11 +527,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     }
     if (stamps) st_prev = __builtin_amdgcn_s_memtime();
 
-    for (int k = 0; k < ntiles; ++k) {
+    for (int k = T_walk; k < T_end; ++k) {
         const int t0 = k * kTile;
         // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
         // (tile k+1) on every wave, balanced dynamically
-        if ((helper || dstw) && k + 2 < ntiles && !BT_ABL(g, 1)) {
+        if ((helper || dstw) && k + 2 < T_end && !BT_ABL(g, 1)) {
             // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
             if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
             const int s = (k + 2) % kStages;
@@ -446,6 +544,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         }
         BT_STAMP(0)
         // ---- stage 3 (tile k)
+        if (SEG && active && k == T_acct && k != T_walk) enter_acct();
         if (active) {
             // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
             // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
@@ -538,7 +637,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
                 asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
                 Fw = 0;
             }
-            sma_flips<PARITY, ONE_TRIP>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
+            sma_flips<PARITY, ONE_TRIP, SEG>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
             BT_STAMP(4)
             if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
                 a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
@@ -551,7 +650,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
             // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
             // zero price), so the uint64 partials are exact as int64
-            if ((k & 1) || k + 1 == ntiles) {
+            if ((k & 1) || k + 1 == T_end) {
                 a.s1 += (i128)(int64_t)a.ps1;
                 a.s2 += (i128)(int64_t)a.ps2;
                 a.ps1 = a.ps2 = 0;
@@ -559,7 +658,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
             BT_STAMP(5)
             if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < ntiles && !BT_ABL(g, 2))
+        if (k + 1 < T_end && !BT_ABL(g, 2))
             stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
                        ctr, (uint32_t)(k + 1), nwaves, lane);
         BT_STAMP(1)
@@ -571,6 +670,40 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         unsigned long long* d = out.dbg + (helper ? 8 : 0);
         for (int i = 0; i < 7; ++i) atomicAdd(&d[i], (unsigned long long)st_acc[i]);
         atomicAdd(&d[7], 1ULL);
+    }
+    if (SEG) {
+        if (active) {
+            SmaSegRec r;
+            r.ntr = a.ntr;
+            r.e0 = a.e0;
+            r.start_pos = start_pos;
+            r.end_pos = a.pos;
+            r.end_e = a.carried ? -1 : a.e;
+            r.end_ce = a.ce;
+            r.x1 = a.x1;
+            r.px1 = a.px1;
+            const Agg g1 = a.x1 >= 0 ? a.agg1 : a.agg;  // carried through: its path so far
+            r.agg1[0] = g1.mx;
+            r.agg1[1] = g1.mn;
+            r.agg1[2] = g1.dd;
+            r.agg1[3] = g1.du;
+            r.end_agg[0] = a.agg.mx;
+            r.end_agg[1] = a.agg.mn;
+            r.end_agg[2] = a.agg.dd;
+            r.end_agg[3] = a.agg.du;
+            r.R = a.R;
+            r.A = a.A;
+            r.B = a.Bq;
+            r.C = a.C;
+            r.D = a.D;
+            r.h = a.h;
+            r.s1lo = (uint64_t)a.s1;
+            r.s1hi = (int64_t)(a.s1 >> 64);
+            r.s2lo = (uint64_t)a.s2;
+            r.s2hi = (int64_t)(a.s2 >> 64);
+            *mine = r;
+        }
+        return;
     }
     if (active) {
         const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
@@ -590,6 +723,94 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
         if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
     }
     wave_add_trades(out, active ? a.ntr : 0);
+}
+
+template <bool PARITY, bool STAMPS, bool ONE_TRIP>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(
+    const SymDesc* __restrict__ syms, const int32_t* __restrict__ close, Grid g, Out out,
+    int dedicated) {
+    sma_body<PARITY, STAMPS, ONE_TRIP, false>(syms, close, g, out, dedicated, SegArgs{}, 0);
+}
+
+// Bar segments (SMA_SEG): its own kernel, for one-block-per-CU shapes (up to 128 VGPRs).
+template <bool ONE_TRIP>
+__global__ __launch_bounds__(1024) void sma_seg_kernel(const SymDesc* __restrict__ syms,
+                                                       const int32_t* __restrict__ close, Grid g,
+                                                       Out out, int dedicated, SegArgs sg,
+                                                       int fix_seg) {
+    sma_body<false, false, ONE_TRIP, true>(syms, close, g, out, dedicated, sg, fix_seg);
+}
+
+// Folds the segments of every (symbol, param) in order (internal.h SmaSegRec): the trade open
+// across a boundary is closed here, with its entry from the segment that opened it and its path
+// merged over the segments it spans; the other trades' sums add and their drawdown forms compose.
+__global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict__ syms, int n_sym,
+                                                       int P, const SmaSegRec* __restrict__ rec,
+                                                       int G, double sqrt_ann, Out out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t n = (size_t)n_sym * P;
+    int ntr = 0;
+    if (i < n) {
+        const int s = (int)(i / P);
+        int32_t pos = 0, e = 0, ce = 0, e0 = -1;
+        Agg agg = kAggId;
+        int64_t R = 0, gap = 0, mdd = 0;
+        uint64_t h = 0;
+        i128 s1 = 0, s2 = 0;
+        for (int q = 0; q < G; ++q) {
+            const SmaSegRec& r = rec[(size_t)q * n + i];
+            ntr += r.ntr;
+            R += r.R;
+            h += r.h;
+            s1 += (i128)(((unsigned __int128)(uint64_t)r.s1hi << 64) | r.s1lo);
+            s2 += (i128)(((unsigned __int128)(uint64_t)r.s2hi << 64) | r.s2lo);
+            if (e0 < 0) e0 = r.e0;
+            const Agg a1 = Agg{r.agg1[0], r.agg1[1], r.agg1[2], r.agg1[3]};
+            if (pos != 0) {
+                if (r.x1 >= 0) {  // the carried trade closes in this segment, before its others
+                    const Agg st = agg_merge(agg, a1);
+                    const bool lg = pos > 0;
+                    const int32_t lo = lg ? st.mn - ce : ce - st.mx;
+                    const int32_t hi = lg ? st.mx - ce : ce - st.mn;
+                    const int32_t path = lg ? st.dd : st.du;
+                    const int32_t pnl = lg ? r.px1 - ce : ce - r.px1;
+                    mdd = max(mdd, max(gap - (int64_t)lo, (int64_t)path));
+                    gap = max(gap, (int64_t)hi) - pnl;
+                    R += pnl;
+                    h += trade_mix((uint64_t)(uint32_t)e | ((uint64_t)(uint32_t)r.x1 << 31) |
+                                   ((uint64_t)lg << 62));
+                } else {
+                    agg = agg_merge(agg, a1);
+                }
+            }
+            mdd = max(mdd, max(gap + r.C, r.D));
+            gap = max(gap + r.A, r.B);
+            if (r.end_pos == 0) {
+                pos = 0;
+            } else if (r.end_e >= 0) {  // a trade opened in this segment is open at its end
+                pos = r.end_pos;
+                e = r.end_e;
+                ce = r.end_ce;
+                agg = Agg{r.end_agg[0], r.end_agg[1], r.end_agg[2], r.end_agg[3]};
+            }
+        }
+        const int B = syms[s].bars;
+        const uint64_t s1lo = (uint64_t)s1, s2lo = (uint64_t)s2;
+        const int64_t s1hi = (int64_t)(s1 >> 64), s2hi = (int64_t)(s2 >> 64);
+        const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, B, sqrt_ann);
+        bt_summary r;
+        r.n_trades = ntr;
+        r.status = 0;
+        r.pnl = R;
+        r.mdd = mdd;
+        r.exposure = ntr > 0 ? B - 1 - e0 : 0;
+        r.sharpe = sh;
+        r.hash = h;
+        out.sum[i] = r;
+        out.key[i] = order_key(sh);
+        if (out.sums != nullptr) out.sums[i] = bt_sums{s1lo, s1hi, s2lo, s2hi};
+    }
+    wave_add_trades(out, ntr);
 }
 
 size_t sma_lds_bytes(const Grid& g) { return sma_lds_layout(g.ring, g.na + g.nb).total; }
@@ -613,8 +834,29 @@ SmaShape sma_shape(int P) {
     return s;
 }
 
+// Bar segments for a shard of one-block-per-CU symbols (16-wave blocks: config 5) that fills the
+// GPU only a few times over: block times vary with each symbol's trade count, so the launch ends
+// with the CU whose few blocks took longest (config 5's 1,250-symbol 8-GPU shard: 4.9 blocks per
+// CU, 121 us per symbol against 107 at 10,000 symbols). Cutting each symbol into G segments gives
+// G times as many, shorter blocks. A segment costs its burn-in tiles and a ring-only lookback
+// over the longest window (about a twentieth of a tile each): G is kept where that stays under 2 %
+// of a segment. Shapes of several blocks per CU (config 2) keep G = 1.
+int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int32_t wmax,
+                          int32_t burn_tiles) {
+    if (n_sym <= 0) return 1;
+    const SmaShape sh = sma_shape(n_params);
+    if (sh.block <= 512) return 1;
+    const double rounds = (double)n_sym * sh.gy / device_cus();
+    if (rounds >= 16.0) return 1;
+    int G = std::min(4, (int)std::ceil(16.0 / rounds));
+    const int ntiles = (max_bars + kTile - 1) / kTile;
+    const int lookback = (wmax - 1 + kTile - 1) / kTile;
+    while (G > 1 && burn_tiles + 0.05 * lookback > 0.02 * ntiles / G) --G;
+    return G;
+}
+
 hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                      const Out& out, bool parity, hipStream_t st) {
+                      const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
     const SmaShape sh = sma_shape(g.n_params);
     const dim3 grid(n_sym, sh.gy), block(sh.block);
@@ -630,6 +872,21 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
         return hipGetLastError();
     }
 #endif
+    if (seg.G > 1 && !parity) {
+        // speculative segments, the fix pass of each boundary in order (a block returns at once
+        // when every lane started in the true position), then the fold
+        const dim3 sgrid(n_sym, sh.gy, seg.G), fgrid(n_sym, sh.gy, 1);
+        for (int s = 0; s < seg.G; ++s) {
+            if (one_trip)
+                hipLaunchKernelGGL((sma_seg_kernel<true>), s == 0 ? sgrid : fgrid, block, lds, st, syms, close, g, out, sh.dedicated, seg, s);
+            else
+                hipLaunchKernelGGL((sma_seg_kernel<false>), s == 0 ? sgrid : fgrid, block, lds, st, syms, close, g, out, sh.dedicated, seg, s);
+        }
+        const size_t n = (size_t)n_sym * g.n_params;
+        hipLaunchKernelGGL(sma_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym,
+                           g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec), seg.G, g.sqrt_ann, out);
+        return hipGetLastError();
+    }
     if (parity && one_trip)
         hipLaunchKernelGGL((sma_kernel<true, false, true>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     else if (parity)

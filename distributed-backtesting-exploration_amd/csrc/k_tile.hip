@@ -52,8 +52,9 @@ struct TileLds {
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
-// per side: nsl + ntp)
-__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0) {
+// per side: nsl + ntp; nsplit finder / accountant pairs of a split walk, 1 or 2)
+__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0,
+                                                  int nsplit = 1) {
     TileLds L{};
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
@@ -72,8 +73,9 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.levp = take((size_t)3 * 2 * nlev * kTile * 4);  // the levels (int32), [tile % 3][side][level][bar]
         L.levf = take((size_t)2 * nlev * 8);         // level factors per side
         L.lvb = take((size_t)(nlev + 1) * 4);        // distinct SL/TP bps, then their count
-        L.rec = take((size_t)2 * kRecCap * kTile * 2);  // trade records [tile & 1][record][lane]
-        L.nrec = take((size_t)2 * kTile);                // records per lane [tile & 1][lane]
+        // trade records [pair][tile & 1][record][lane] and records per lane [pair][tile & 1][lane]
+        L.rec = take((size_t)nsplit * 2 * kRecCap * kTile * 2);
+        L.nrec = take((size_t)nsplit * 2 * kTile);
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
@@ -635,13 +637,19 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          const int32_t* __restrict__ close,
                                                          Grid g, Out out, int nextra, int lpw,
                                                          SegArgs sg, int fix_seg, int split_grp,
-                                                         uint32_t wave_map) {
+                                                         int split_grp2, uint32_t wave_map) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
     const int nsl = g.nc, ntp = g.nd, nlev = nsl + ntp;
-    const TileLds LL = tile_lds_layout(1, R, nw, nk, nlev);
-    uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);                    // sum c
-    unsigned __int128* r2 = reinterpret_cast<unsigned __int128*>(smem + LL.r2);  // sum c^2
+    // finder / accountant pairs: parameter groups split_grp and (if >= 0) split_grp2
+    const int nsplit = split_grp < 0 ? 0 : (split_grp2 < 0 ? 1 : 2);
+    const TileLds LL = tile_lds_layout(1, R, nw, nk, nlev, nsplit > 0 ? nsplit : 1);
+    // prefix rings as exact doubles (every prefix < 2^53 for series up to kMaxBars = 2^22 bars):
+    // sum c, and sum c^2 split at bit 31 into sum (c^2 >> 31) and sum (c^2 & (2^31 - 1)), so
+    // a window's S1 and the two halves of S2 are exact double differences and S2 = hi 2^31 + lo
+    // rounds once, with no int64 / int128 arithmetic or conversion per window task
+    double* r1 = reinterpret_cast<double*>(smem + LL.r1);     // sum c
+    double2* r2 = reinterpret_cast<double2*>(smem + LL.r2);   // {sum c^2 >> 31, sum c^2 & 2^31-1}
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
@@ -670,17 +678,24 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // indices), so the heavy roles land on different SIMDs next to light ones
     const int tid = threadIdx.x, lane = tid & 63, hw_wave = tid >> 6;
     const int wave = hw_wave < 8 ? (int)((wave_map >> (4 * hw_wave)) & 15u) : hw_wave;
-    // waves: [0, npw) parameter groups, npw the helper, npw + 1 the accountant of a split walk,
-    // then `nextra` task-only waves. Without a split every parameter wave walks and accounts its
-    // lanes' trades (walker); with one, parameter wave split_grp (the group of the busiest z
-    // threshold, whose per-lane trade chain sets the tile time) only finds its trades
-    // (finder) and the accountant wave keeps their accounts, one tile behind.
-    const bool split = split_grp >= 0;
-    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra - (split ? 1 : 0);
+    // waves: [0, npw) parameter groups, npw the helper, npw + 1 .. npw + nsplit the accountants
+    // of a split walk, then `nextra` task-only waves. Without a split every parameter wave walks
+    // and accounts its lanes' trades (walker); with one, parameter wave split_grp (the group of
+    // the busiest z threshold, whose per-lane trade chain sets the tile time) only finds its
+    // trades (finder) and the accountant wave keeps their accounts, one tile behind; with two,
+    // the group of the second-busiest threshold (split_grp2) is split the same way.
+    const bool split = nsplit > 0;
+    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra - nsplit;
     const bool helper = wave == npw;
-    const bool accountant = split && wave == npw + 1;
-    const bool finder = split && wave == split_grp;
-    const int grp = accountant ? split_grp : wave;
+    const int acc_i = wave - npw - 1;
+    const bool accountant = split && acc_i >= 0 && acc_i < nsplit;
+    const int fin_i = wave == split_grp ? 0 : (wave == split_grp2 ? 1 : -1);
+    const bool finder = split && fin_i >= 0;
+    const int grp = accountant ? (acc_i == 0 ? split_grp : split_grp2) : wave;
+    // this wave's record buffers (finder and accountant of one pair share them)
+    const int pair = accountant ? acc_i : (finder ? fin_i : 0);
+    recs += (size_t)pair * 2 * kRecCap * kTile;
+    nrec += (size_t)pair * 2 * kTile;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
     const int j = (blockIdx.y * npw + grp) * lpw + lane;
@@ -730,8 +745,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     auto task_count = [&](int nu) { return nw + 2 * ((nu + kLevPass - 1) / kLevPass); };
     if (tid == 0) {
         // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
-        r1[(T_scan * kTile) % R] = 0;
-        r2[(T_scan * kTile) % R] = 0;
+        r1[(T_scan * kTile) % R] = 0.0;
+        r2[(T_scan * kTile) % R] = double2{0.0, 0.0};
         // the distinct SL/TP distances (a level 1e4 -+ bps is shared by every SL and TP of that
         // bps: config 4's {50, 100} and {50, 100, 200, 400} make 4 levels per side, not 6) and
         // their factors (level_y)
@@ -763,7 +778,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int lev_lo_long = usl, lev_lo_short = utp, lev_hi_long = utp, lev_hi_short = usl;
 
     TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
-    unsigned __int128 cy2 = 0;
+    int64_t cy2h = 0, cy2l = 0;  // sums of c^2 >> 31 and c^2 & (2^31 - 1) before the tile
     int32_t cpre = 0, hpre = 0, lpre = 0;
 
     auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
@@ -771,14 +786,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy);
         const int pt = ring_pos(T, lane, R);
-        r1[pt] = (uint64_t)pre;
-        // sum of c^2 in 128 bits: scan the 32-bit halves of c^2 < 2^62 separately
+        r1[pt] = (double)pre;  // exact: < 2^31 x 2^22 bars
+        // sum of c^2 (< 2^62) as its parts above and below bit 31, each prefix < 2^53
         const uint64_t c2 = (uint64_t)((int64_t)c * c);
-        const int64_t slo = wave_iscan_i64((int64_t)(c2 & 0xFFFFFFFFu));
-        const int64_t shi = wave_iscan_i64((int64_t)(c2 >> 32));
-        const unsigned __int128 inc2 = ((unsigned __int128)(uint64_t)shi << 32) + (uint64_t)slo;
-        r2[pt] = cy2 + inc2;
-        cy2 += ((unsigned __int128)(uint64_t)lane63_i64(shi) << 32) + (uint64_t)lane63_i64(slo);
+        const int64_t slo = wave_iscan_i64((int64_t)(c2 & 0x7FFFFFFFu));
+        const int64_t shi = wave_iscan_i64((int64_t)(c2 >> 31));
+        r2[pt] = double2{(double)(cy2h + shi), (double)(cy2l + slo)};
+        cy2h += lane63_i64(shi);
+        cy2l += lane63_i64(slo);
         // raw lows / highs and their 8-bar block extrema
         int32_t* LH = lhs_ + s * kLH;
         LH[lane] = lv;
@@ -850,8 +865,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int64_t c = cts[s * kTile + lane];
         uint64_t* Wd = words + (T & 1) * nword;
         const int ptop = ring_pos(T, lane, R);
-        const uint64_t P1t = r1[ptop];
-        const unsigned __int128 P2t = r2[ptop];
+        const double P1t = r1[ptop];
+        const double2 P2t = r2[ptop];
+        const double cdw = (double)c;
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
@@ -889,31 +905,32 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
             const int pj = ring_back(ptop, Wn, R);
-            // window sums: S1 = sum c in [0, 2^44) (prices < 2^31, windows < 2^13), S2 = sum c^2
-            const uint64_t S1 = P1t - r1[pj];
-            const unsigned __int128 S2 = P2t - r2[pj];
-            const int64_t Dv = (int64_t)Wn * c - (int64_t)S1;
-            // Q = W S2 - S1^2 in fp64 with a proven bracket: S1 < 2^44 converts exactly, S2 <
-            // 2^75 rounds once, the product, the square and the difference once each, and S1^2 <=
-            // W S2, so |Qd - Q| < 2^-50 pd (pd = W S2 rounded). Qd -/+ 2^-48 pd then brackets Q
-            // with room for the roundings of the bracket and of the k^2 products below.
-            const double S2d = (double)(uint64_t)(S2 >> 32) * 0x1p32 + (double)(uint32_t)S2;
-            const double S1d = (double)S1;
-            const double pd = (double)Wn * S2d;
+            // window sums: S1 = sum c < 2^47 (prices < 2^31, windows <= 2^16) and the two parts
+            // of S2 = sum c^2: exact differences of the exact prefix doubles; D = W c - S1 is
+            // exact too (W c < 2^47)
+            const double2 q2 = r2[pj];
+            const double S1d = P1t - r1[pj];
+            const double dH = P2t.x - q2.x, dL = P2t.y - q2.y;
+            const double wlen = (double)Wn;
+            const double Dd = wlen * cdw - S1d;
+            // Q = W S2 - S1^2 in fp64 with a proven bracket: S1 is exact, S2 = dH 2^31 + dL
+            // (< 2^79) rounds once, the product, the square and the difference once each, and
+            // S1^2 <= W S2, so |Qd - Q| < 2^-50 pd (pd = W S2 rounded). Qd -/+ 2^-48 pd then
+            // brackets Q with room for the roundings of the bracket and of the k^2 products below.
+            const double S2d = dH * 0x1p31 + dL;
+            const double pd = wlen * S2d;
             const double Qd = pd - S1d * S1d;
             // with lh's own margin folded in (lh is within 2^-51 of L; 2^-47 covers both)
             const double QH = (Qd + pd * 0x1p-48) * (1.0 + 0x1p-47);
             const double QL = (Qd - pd * 0x1p-48) * (1.0 - 0x1p-47);
-            // fp64 fast path: |z| > k <=> L = Dv^2 kd^2 > R = kn^2 Q. |Dv| < 2^53 converts exactly
-            // and lh is within 2^-51 of L; after rounding lh > kn^2 QH proves L > R and
-            // kn^2 QL > lh proves L < R. A valid lane with neither (both sides zero included, or a
-            // window so flat that Q is inside the bracket) is settled exactly in int128 with its
-            // whole wave.
-            const double Dd = (double)Dv;
+            // fp64 fast path: |z| > k <=> L = D^2 kd^2 > R = kn^2 Q. D is exact and lh is within
+            // 2^-51 of L; after rounding lh > kn^2 QH proves L > R and kn^2 QL > lh proves L < R.
+            // A valid lane with neither (both sides zero included, or a window so flat that Q is
+            // inside the bracket) is settled exactly in int128 with its whole wave.
             const double lh = (Dd * Dd) * kd2d;
             const uint64_t vm = ballot(valid);
-            const uint64_t dp = ballot(valid && Dv >= 0), dn = ballot(valid && Dv <= 0);
-            const uint64_t zneg = vm & ~dp, zpos = vm & ~dn;  // Dv < 0, Dv > 0
+            const uint64_t dp = ballot(valid && Dd >= 0.0), dn = ballot(valid && Dd <= 0.0);
+            const uint64_t zneg = vm & ~dp, zpos = vm & ~dn;  // D < 0, D > 0
             // z tests of one k: lane 4 qq .. 4 qq + 3 of `zw` collect its words (v_writelane, lane
             // = dword of Wd[2 (ow nk + q) + side]), one store per pass of kMaxK values; a
             // lane the fp64 bracket cannot settle marks the k in `unc` (wave-uniform), and the
@@ -930,8 +947,15 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 writelane<4 * qq + 3>(zw, (uint32_t)(zh >> 32));
             };
             auto settle = [&](int q0, uint32_t unc, uint32_t& zw) {  // rare
-                const uint64_t S1x = P1t - r1[pj];
-                const unsigned __int128 S2x = P2t - r2[pj];
+                // the exact integers behind the doubles, re-read from the rings (nothing stays live
+                // across the tests for this rare path); lanes outside the window are masked by
+                // `valid`, their values are never used
+                const double2 r2x = r2[pj];
+                const double S1e = P1t - r1[pj];
+                const uint64_t S1x = valid ? (uint64_t)S1e : 0;
+                const int64_t Dv = valid ? (int64_t)((double)Wn * cdw - S1e) : 0;
+                const unsigned __int128 S2x =
+                    valid ? ((unsigned __int128)(uint64_t)(P2t.x - r2x.x) << 31) + (uint64_t)(P2t.y - r2x.y) : 0;
                 const unsigned __int128 Q = mul_u128_u32(S2x, (uint32_t)Wn) - sq_u64(S1x);
 #pragma unroll 1
                 while (unc) {
@@ -1279,7 +1303,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     if (STAMPS && blockIdx.x == 0 && blockIdx.z == 0 && lane == 0 && hw_wave < 8 && out.dbg != nullptr)
         out.dbg[56 + hw_wave] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) + 1;
     if (SEG) {
-        if (keeps) seg_write(a, start_pos, start_e, mine);
+        // the record's address again (keeping `mine` live across the whole walk costs a VGPR pair
+        // at the 128-register edge)
+        int pje = pj;
+        asm volatile("" : "+v"(pje));  // opaque: the address is not merged with `mine`
+        if (keeps) seg_write(a, start_pos, start_e, sg.rec + (size_t)sr.seg * gridDim.x * P + (size_t)blockIdx.x * P + pje);
         return;
     }
     if (keeps) acct_write(a, B, g.sqrt_ann, gi, out);
@@ -1348,16 +1376,19 @@ static int tile_param_waves(int need, int cap) {
 // runs on SIMD w % 4, so waves w and w + 4 share one: each busy parameter wave (the walks, the
 // busiest first) gets a task-only wave as its partner (task waves take fewer tasks when their
 // SIMD is busy), the lightest parameter wave the helper, and the accountant of a split walk a
-// light parameter wave. Identity for blocks other than 8 waves.
-static uint32_t boll_wave_map(int pw, int split_grp, int xw) {
+// light parameter wave. With two split pairs (finders in groups 0 and 1) the heavy roles —
+// accountant 0, finder 0, the helper, accountant 1 — each get a SIMD, next to the light walkers,
+// finder 1 and the task wave. Identity for other block shapes.
+static uint32_t boll_wave_map(int pw, int nsplit, int split_grp, int split_grp2, int xw) {
     uint32_t m = 0;
     for (int w = 0; w < 8; ++w) m |= (uint32_t)w << (4 * w);
-    const int nw = pw + 1 + (split_grp >= 0 ? 1 : 0) + xw;
-    if (nw == 8 && pw == 4) {
-        // logical roles: 0-3 parameter groups, 4 helper, then (split) 5 accountant, then tasks
+    const int nw = pw + 1 + nsplit + xw;
+    if (nw == 8 && pw == 4 && (nsplit < 2 || (split_grp == 0 && split_grp2 == 1))) {
+        // logical roles: 0-3 parameter groups, 4 helper, then the accountants, then tasks
+        const int split2_map[8] = {5, 0, 4, 6, 3, 2, 1, 7};
         const int split_map[8] = {0, 1, 2, 3, 6, 7, 5, 4};
         const int plain_map[8] = {0, 1, 2, 3, 5, 6, 7, 4};
-        const int* r = split_grp >= 0 ? split_map : plain_map;
+        const int* r = nsplit == 2 ? split2_map : (nsplit == 1 ? split_map : plain_map);
         m = 0;
         for (int w = 0; w < 8; ++w) m |= (uint32_t)r[w] << (4 * w);
     }
@@ -1377,6 +1408,20 @@ static bool tile_split_walk() {
     return on;
 }
 
+// Second finder/accountant pair (the second-busiest z threshold): off unless built with
+// -DBT_SPLIT2 (A/B build) or, in the profiling build, BT_SPLIT2=1.
+static bool tile_split_walk2() {
+#ifdef BT_SPLIT2
+    bool on = true;
+#else
+    bool on = false;
+#endif
+#ifdef BT_PROFILING
+    if (const char* v = getenv("BT_SPLIT2")) on = atoi(v) != 0;
+#endif
+    return on;
+}
+
 static int tile_lanes_per_wave() {
     int l = 64;
 #ifdef BT_PROFILING
@@ -1386,7 +1431,7 @@ static int tile_lanes_per_wave() {
 }
 
 // Compute units of the current device (one process per GPU).
-static int device_cus() {
+int device_cus() {
     static int n = 0;
     if (n <= 0) {
         int dev = 0;
@@ -1405,7 +1450,9 @@ static int tile_extra_waves(int used, int x) {
 }
 
 size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
-size_t boll_lds_bytes(const Grid& g) { return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd).total; }
+size_t boll_lds_bytes(const Grid& g, int nsplit) {
+    return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd, nsplit).total;
+}
 
 int32_t ema_burn_tiles(int32_t max_span) {
     // two fp64 EMA chains from different starts met bit for bit after 131-162 bars (span 10)
@@ -1482,39 +1529,53 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     // the most, and its lanes' serial trade chains set the tile time (config 4: 7.1 walk
     // iterations per tile against 1.0-4.3 for the other waves), so that wave only finds trades
     // and an accountant wave keeps their accounts a tile later.
-    int split_grp = -1;
+    int split_grp = -1, split_grp2 = -1;
     if (tile_split_walk() && pw >= 2 && grid.y == 1) {
-        const int grp = (int)(((long long)g.kmin_idx * g.na * g.nc * g.nd) / lpw);
+        const long long per_k = (long long)g.na * g.nc * g.nd;  // lanes per z threshold
+        const int grp = (int)((g.kmin_idx * per_k) / lpw);
         if (grp < pw) split_grp = grp;
+        // the second-smallest threshold trades next most (config 4: 4.3 walk iterations per
+        // tile against 7.1 for the smallest, 1.0-1.3 for the others): its own finder/accountant
+        // pair, when its group is another wave and the records of both pairs leave two blocks'
+        // LDS on a CU (k values beyond the first 8 are not ranked: kn2 holds 8)
+        int k2 = -1;
+        for (int q = 0; q < std::min(g.nb, 8); ++q)
+            if (q != g.kmin_idx && (k2 < 0 || g.kn2[q] < g.kn2[k2])) k2 = q;
+        const int grp2 = k2 >= 0 ? (int)((k2 * per_k) / lpw) : -1;
+        if (split_grp >= 0 && tile_split_walk2() && pw >= 4 && grp2 >= 0 && grp2 < pw &&
+            grp2 != split_grp && boll_lds_bytes(g, 2) <= 80 * 1024)
+            split_grp2 = grp2;
     }
-    const int base = pw + 1 + (split_grp >= 0 ? 1 : 0);
+    const int nsplit = split_grp < 0 ? 0 : (split_grp2 < 0 ? 1 : 2);
+    const int base = pw + 1 + nsplit;
     // at most one block per CU (config 4 on 8 GPUs: 250 symbols) leaves wave slots free: four
     // task-only waves (8.17 -> 7.90 ms vs two); otherwise as many as keep the block at 8 waves,
-    // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms)
+    // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms;
+    // with two split pairs one task wave is left)
     const bool sparse = (long long)grid.x * grid.y * grid.z <= device_cus();
-    const int xw = tile_extra_waves(base, sparse ? 4 : std::max(2, std::min(3, 8 - base)));
+    const int xw = tile_extra_waves(base, sparse ? 4 : std::max(nsplit == 2 ? 1 : 2, std::min(3, 8 - base)));
     const dim3 block(64 * (base + xw));
-    const size_t lds = boll_lds_bytes(g);
-    const uint32_t wmap = boll_wave_map(pw, split_grp, xw);
+    const size_t lds = boll_lds_bytes(g, nsplit > 0 ? nsplit : 1);
+    const uint32_t wmap = boll_wave_map(pw, nsplit, split_grp, split_grp2, xw);
 #ifdef BT_PROFILING
     if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
         return hipGetLastError();
     }
 #endif
     if (split) {
         // speculative segments, then the fix pass of each boundary in order (a block returns at
         // once when its lanes' starts were right), then the fold
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
         const dim3 fgrid(grid.x, grid.y, 1);
         for (int s = 1; s < seg.G; ++s)
-            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s, split_grp, wmap);
+            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s, split_grp, split_grp2, wmap);
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
     } else if (parity) {
-        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
     } else {
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
     }
     return hipGetLastError();
 }

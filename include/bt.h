@@ -134,11 +134,13 @@ void bt_engine_destroy(bt_engine* e);
 const char* bt_last_error(void);      /* thread-local message of the last failed call */
 int32_t bt_abi_version(void);
 int32_t bt_num_params(const bt_engine* e);
-/* Bar-axis split of the EMA+OLS and Bollinger walks (k_tile.hip; small shards): segments per
- * symbol (0 = automatic: split when the shard has no more workgroups than the GPU has CUs;
- * 1 = never; n = always n) and the burn-in tiles a speculative segment walks before its first bar
- * (0 = the default: 64 for Bollinger, 24 x the longest span for EMA+OLS, so every fp64 EMA chain
- * meets the true one). Results are identical either way (a boundary whose speculative start differs from
+/* Bar-axis split of every strategy's walk (k_tile.hip, k_sma.hip): segments per symbol (0 =
+ * automatic: EMA+OLS and Bollinger split a shard with no more workgroups than the GPU has CUs, SMA
+ * a shard of one-block-per-CU symbols that fills the GPU fewer than 16 times; 1 = never; n =
+ * always n) and the burn-in tiles a speculative segment walks before its first bar (0 = the
+ * default: 64 for Bollinger, 24 x the longest span for EMA+OLS, so every fp64 EMA chain meets the
+ * true one, 2 for SMA, whose trade open at a boundary is carried symbolically into a combine
+ * pass). Results are identical either way (a boundary whose speculative start differs from
  * the true one is re-walked); parity mode (trade lists) never splits. bt_last_segments: the count
  * the last bt_run used and, if refixed_blocks is not NULL, how many (symbol, boundary) blocks the
  * fix pass re-walked (waits for the run). */

@@ -69,6 +69,8 @@ def test_config5_full_shard():
         e.load_synthetic(SEED, 3750, S, bars, D.BT_MINUTE)   # the shard of rank 3 of 8
         e.run()
         allr, st, top = e.summaries(), e.stats(), e.read_topk()
+        used = e.last_segments()
+    assert used > 1  # the 8-GPU shard fills the GPU ~5 times: automatic bar segments (k_sma.hip)
     assert all(3750 <= int(t["sym"]) < 5000 for t in top)   # global symbol ids
     top_local = top.copy()
     top_local["sym"] -= 3750

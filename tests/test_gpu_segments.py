@@ -174,18 +174,94 @@ def test_ema_auto_split_config3_grid_small_shard():
             compare_summary(got[s, p], orc[p], f"ema auto split sym {200 + s} {grid.param(p)}")
 
 
+SMA_SEG_GRID = lambda: D.Grid.sma([5, 20, 60, 150], [200, 900, 3000], annualization=98280)
+
+
+@pytest.mark.parametrize("segments,burn", [(2, 2), (3, 1), (4, 1), (6, 3)])
+def test_sma_split_equals_unsplit_and_oracle(segments, burn):
+    """SMA bar segments (k_sma.hip SEG): positions are held for thousands of bars, so the trade
+    open at a boundary is carried symbolically and closed by the combine pass. Every summary
+    field equals the unsplit kernel and the oracle bit for bit."""
+    grid = SMA_SEG_GRID()
+    cols = [F.gen(0x5EED, 500 + i, 30000 + 7000 * i, 1) for i in range(3)]
+    ref, used1, _ = _run_grid(grid, cols, 1)
+    got, used, _ = _run_grid(grid, cols, segments, burn)
+    assert used1 == 1 and used == segments
+    assert got.tobytes() == ref.tobytes(), "split run differs from the unsplit run"
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("sma", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(grid.n_params):
+            compare_summary(got[i, p], orc[p], f"sma G={segments} burn={burn} sym {i} {grid.param(p)}")
+
+
+def test_sma_split_ragged_and_empty_segments():
+    grid = D.Grid.sma([2, 3, 10], [4, 70, 200], annualization=98280)
+    lengths = [1, 2, 63, 64, 65, 130, 700, 5000]
+    cols = [F.gen(0x5EED, 90 + i, n, 1) for i, n in enumerate(lengths)]
+    ref, _, _ = _run_grid(grid, cols, 1)
+    for segments, burn in ((4, 1), (9, 1), (3, 2)):
+        got, used, _ = _run_grid(grid, cols, segments, burn)
+        assert used == segments and got.tobytes() == ref.tobytes(), (segments, burn)
+    for i, x in enumerate(cols):
+        orc, _ = oracle_row("sma", grid, (x[0], x[1], x[2], x[3]), 98280)
+        for p in range(grid.n_params):
+            compare_summary(ref[i, p], orc[p], f"sma ragged {lengths[i]} bars {grid.param(p)}")
+
+
+def test_sma_split_tied_burn_in_takes_the_fix_pass():
+    """Flat prices across the boundaries: every comparison of the burn-in ties, so a speculative
+    segment starts flat while the true position (set before the flat stretch) is held; the fix
+    pass re-walks those segments from the true position."""
+    grid = D.Grid.sma([3, 8, 20], [40, 90], annualization=98280)
+    rng = np.random.default_rng(11)
+    walk = lambda n, c0: np.clip(c0 + np.cumsum(rng.integers(-3000, 3001, n)), 10_000, 2**31 - 1)
+    a = walk(5000, 1_000_000)
+    c = np.concatenate([a, np.full(10000, a[-1]), walk(5000, a[-1])]).astype(np.int32)
+    cols = [(c, c, c, c)]
+    ref, _, _ = _run_grid(grid, cols, 1)
+    got, used, refixed = _run_grid(grid, cols, 3, 1)   # boundaries at bars 6,720 and 13,376
+    assert used == 3 and refixed > 0
+    assert got.tobytes() == ref.tobytes()
+    orc, _ = oracle_row("sma", grid, (c, c, c, c), 98280)
+    for p in range(grid.n_params):
+        compare_summary(got[0, p], orc[p], f"sma flat boundary {grid.param(p)}")
+
+
+def test_sma_auto_segments_only_for_few_long_blocks():
+    """Automatic mode splits the config-5 shape (16-wave blocks, a shard filling the GPU a few
+    times) and leaves config 2 (several 8-wave blocks per CU) alone."""
+    with D.Engine(D.config2_grid()) as e:
+        e.load_synthetic(0x5EED, 0, 600, 2520, D.BT_DAILY)
+        e.run()
+        assert e.last_segments() == 1
+    with D.Engine(D.config5_grid()) as e:
+        e.load_synthetic(0x5EED, 0, 300, 60000, D.BT_MINUTE)
+        e.run()
+        assert e.last_segments() > 1
+        got = e.summaries().copy()
+    closes = np.stack([F.gen(0x5EED, s, 60000, 1)[3] for s in (0, 299)])
+    grid = D.config5_grid()
+    orc = F.sma_grid_mt(closes, np.asarray(grid.axes[0]), np.asarray(grid.axes[1]), 98280, 8)
+    for i, s in enumerate((0, 299)):
+        for p in range(grid.n_params):
+            compare_summary(got[s, p], orc[i, p], f"config-5 grid auto split sym {s} param {p}")
+
+
 _NS = int(__import__("os").environ.get("BT_RANDOM_SEEDS", "0"))
 
 
-@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("boll", "ema_ols") for s in range(_NS or 3)])
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("boll", "ema_ols", "sma") for s in range(_NS or 3)])
 def test_random_splits_equal_unsplit(strategy, seed):
-    """Random grids, segment counts (2-6), burn-ins (1-6 tiles) and ragged random-walk series:
+    """Random grids, segment counts (2-6), burn-ins (1-6 tiles) and ragged random-walk series
+    (SMA's symbolic carried trades included):
     the split run equals the unsplit one bit for bit (the unsplit kernels are oracle-checked by
     the parity sweeps), whether or not the fix pass re-walks boundaries."""
     rng = np.random.default_rng(4000 + seed + (500 if strategy == "ema_ols" else 0))
     pick = lambda lo, hi, k: sorted(int(x) for x in rng.choice(np.arange(lo, hi), k, replace=False))
     if strategy == "boll":
         grid = D.Grid.boll(pick(2, 121, 8), pick(1, 9, 4), pick(10, 300, 2), pick(10, 500, 4), k_den=2)
+    elif strategy == "sma":
+        grid = D.Grid.sma(pick(2, 60, 4), pick(20, 2000, 4), annualization=98280)
     else:
         grid = D.Grid.ema_ols(pick(2, 200, 4), pick(2, 400, 4), band_bps=int(rng.integers(0, 60)))
     n = int(rng.integers(2, 6))
