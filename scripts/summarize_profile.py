@@ -31,7 +31,8 @@ steps = line["steps"]
 # one fix pass per boundary and the combine pass (k_tile.hip): a step's kernel time is the sum
 # of its group of dispatches, the same span the bench line's HIP events bracket.
 def ours(name):
-    return kname in name or "seg_combine" in name
+    # SMA bar segments launch sma_seg_kernel (speculative + fix passes) and sma_seg_combine
+    return kname in name or "seg_combine" in name or (kname == "sma_kernel" and "sma_seg_kernel" in name)
 
 
 rows = list(csv.DictReader(open(glob.glob(f"{src}/trace/*kernel_trace.csv")[0])))
