@@ -275,6 +275,9 @@ def main():
         elapsed = float(tt.item())
     kms, launches, kname = eng.kernel_timing()
     stats = eng.stats()
+    # bar segments per symbol of the last run and the blocks its fix passes re-walked (read
+    # after the timed region: the count is a device read-back)
+    n_seg, refixed = eng.last_segments(with_refixed=True)
 
     if rank == 0:
         evals_per_step = total * BARS * P
@@ -322,6 +325,7 @@ def main():
                          "pmc_source": pmc.get("source") if same_shard else None,
                          "kernel": kname, "kernel_avg_ms": kavg_s * 1e3},
             "trades_per_step": stats["trades"],
+            "bar_segments": {"per_symbol": n_seg, "refixed_blocks_last_step": refixed},
             "top1": {"sharpe": float(top[0]["sharpe"]), "sym": int(top[0]["sym"]),
                      "param": int(top[0]["param"])} if top is not None and len(top) else None,
         }

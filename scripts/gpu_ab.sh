@@ -9,7 +9,7 @@ for r in $(seq ${R:-2}); do
     for c in ${CASES:-4:500}; do
       cfg=${c%%:*}; s=${c##*:}
       BT_LIB=$lib timeout -k 10 200 python3 bench.py --config $cfg --symbols $s --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/ab/b.log 2>&1 || { tail -5 gpurun_out/ab/b.log; exit 1; }
-      python3 -c "import json; d=json.loads(open('gpurun_out/ab/b.log').read().strip().splitlines()[-1]); print('round $r', '$lib', 'config', $cfg, $s, 'kernel', round(d['roofline']['kernel_avg_ms'],4), 'ms/step', round(d['ms_per_step'],4))"
+      python3 -c "import json; d=json.loads(open('gpurun_out/ab/b.log').read().strip().splitlines()[-1]); print('round $r', '$lib', 'config', $cfg, $s, 'kernel', round(d['roofline']['kernel_avg_ms'],4), 'ms/step', round(d['ms_per_step'],4), 'segments', d.get('bar_segments'))"
     done
   done
 done
