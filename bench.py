@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--topk", type=int, default=TOPK,
                     help="0 skips the top-k chain (profiling-build ablations, where Sharpes tie)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="bar segments per symbol (bt_set_segments): 0 = automatic, 1 = off")
+    ap.add_argument("--burn", type=int, default=0,
+                    help="burn-in tiles of a speculative segment: 0 = the strategy's default")
     args = ap.parse_args()
     if args.leg == "ingest":
         return ingest_leg(args)
@@ -207,6 +211,8 @@ def main():
     P = grid.n_params
     topk = args.topk
     eng = D.Engine(grid, device=device, topk=topk, timing=True)
+    if args.segments or args.burn:
+        eng.set_segments(args.segments, args.burn)
     eng.load_synthetic(SEED, sym0, n_sym, BARS, cfg["freq"])
     exchange = "none"
     if dist is not None:

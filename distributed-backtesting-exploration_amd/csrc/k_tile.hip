@@ -195,9 +195,11 @@ __device__ __forceinline__ uint64_t latch64(uint64_t S, uint64_t R, uint64_t q) 
 //           latches' edges, O(1) accounting per trade.
 // SEG: bar segments as in boll_tile_kernel; besides the lanes' trade states a segment's start
 // must agree on the EMA chains: a speculative segment starts each chain at its first scanned bar
-// (e = c there) and records the values entering its first accounted bar; fp64 chains from
-// different starts meet bit for bit after ~16 spans of bars (the burn-in covers 24), after which
-// they are identical. The fix pass compares them too and re-walks from the true values.
+// from an estimate of the true value (a truncated weighted sum of the closes before it, summed in
+// parallel) and records the values entering its first accounted bar; fp64 chains from different
+// starts meet bit for bit once the start's error has decayed below rounding (from the estimate:
+// <= 4 spans of bars; from e = c: ~16), after which they are identical. The fix pass compares
+// them too and re-walks from the true values.
 template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
@@ -254,11 +256,63 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         }
     }
     const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
-    // the chains start at bar chain_b0 with e = c there (bar 0, or a speculative segment's first
-    // scanned bar); the fix pass instead starts them at its first bar from the true values
+    // the chains start at bar 0 with e = c there; a speculative segment's chains continue from
+    // an estimate of the true values entering its first scanned bar, and the fix pass starts
+    // them at its first bar from the true values
     const bool chain_injected = SEG && fix_seg > 0;
-    const int chain_b0 = chain_injected ? -1 : T_scan * kTile;
+    const bool chain_est = SEG && fix_seg == 0 && T_scan > 0;
+    const int chain_b0 = (chain_injected || chain_est) ? -1 : 0;
     const int chain_T0 = chain_injected ? T_acct : T_scan;
+
+    // The estimate: e_ts = sum_{i<M} a (1-a)^i c_{ts-i} + (1-a)^M c_{ts-M+1}, the closed form of
+    // the recurrence truncated after e^-36 of the weight (exact in real arithmetic when M reaches
+    // bar 0). Every wave sums a strided share of the M bars, four spans at a time; the per-wave
+    // sums go to ebuf (free until the first chain tile) and helper B adds them in wave order, so
+    // the estimate is deterministic. Its rounding (~1e-14 relative) dies out in ~4 spans of
+    // bars; the chains then meet the true ones bit for bit, and the fix pass catches any that
+    // do not.
+    int est_M = 0;
+    if (chain_est) {
+        const int ts = T_scan * kTile - 1;
+        int maxspan = 1;
+        for (int q = 0; q < nsp; ++q) maxspan = max(maxspan, g.a[q]);
+        est_M = (int)min((int64_t)ts + 1, (int64_t)18 * ((int64_t)maxspan + 1) + 1);
+        const int nchunk = (est_M + kTile - 1) / kTile;
+        for (int q0 = 0; q0 < nsp; q0 += 4) {
+            double acc[4], w[4], r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = min(q0 + u, nsp - 1);
+                const double a = 2.0 / ((double)g.a[q] + 1.0), lb = log2(1.0 - a);
+                acc[u] = 0.0;
+                w[u] = q0 + u < nsp ? a * exp2(lb * (double)(wave * kTile + lane)) : 0.0;
+                r[u] = exp2(lb * (double)(kTile * nwaves));
+            }
+            for (int ch = wave; ch < nchunk; ch += 8 * nwaves) {
+                int32_t cv[8];
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+                    const int i = (ch + v * nwaves) * kTile + lane;
+                    cv[v] = i < est_M ? crow[ts - i] : 0;
+                }
+#pragma unroll
+                for (int v = 0; v < 8; ++v) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        acc[u] = __builtin_fma(w[u], (double)cv[v], acc[u]);
+                        w[u] *= r[u];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                double s = acc[u];
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+                if (lane == 0 && q0 + u < nsp) ebuf[wave * nsp + q0 + u] = s;
+            }
+        }
+    }
 
     for (int o = tid; o < nol; o += blockDim.x) win[o] = g.b[o];
     if (tid == 0) {
@@ -277,6 +331,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int winreg = lane < nol ? g.b[lane] : 1;  // OLS window lengths, lane = window
     const double lo_mult = (double)(10000 - g.band_bps), hi_mult = (double)(10000 + g.band_bps);
     __syncthreads();
+    if (chain_est && helperB && lane < nsp) {
+        double s = 0.0;
+        for (int w2 = 0; w2 < nwaves; ++w2) s += ebuf[w2 * nsp + lane];
+        const double tail = (double)crow[T_scan * kTile - est_M];
+        ema = s + exp2(log2(1.0 - alpha) * (double)est_M) * tail;
+    }
 
     TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     uint64_t cy2 = 0;
@@ -1455,9 +1515,11 @@ size_t boll_lds_bytes(const Grid& g, int nsplit) {
 }
 
 int32_t ema_burn_tiles(int32_t max_span) {
-    // two fp64 EMA chains from different starts met bit for bit after 131-162 bars (span 10)
-    // to 11,559-13,368 bars (span 780) over 18 starts each (round-2 measurement): 24 spans
-    return std::max(kDefaultBurnTiles, (24 * max_span + kTile - 1) / kTile);
+    // fp64 EMA chains started from e = c met the true ones after 131-162 bars (span 10) to
+    // 11,559-13,368 bars (span 780) over 18 starts each (round-2 measurement); started from the
+    // weighted-sum estimate, after at most 2.6 (span 10) to 3.8 (span 780) spans (round 3,
+    // 18 starts each): 6 spans, on top of the OLS lookback tiles the chain also runs through
+    return std::max(kDefaultBurnTiles, (6 * max_span + kTile - 1) / kTile);
 }
 
 int32_t ema_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int32_t burn_tiles) {

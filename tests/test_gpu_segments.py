@@ -105,8 +105,9 @@ def _run_grid(grid, cols, segments, burn=0):
 @pytest.mark.parametrize("segments,burn", [(2, 0), (3, 0), (2, 1), (4, 2)])
 def test_ema_split_equals_unsplit_and_oracle(segments, burn):
     """EMA+OLS segments must also agree on the fp64 EMA chains at every boundary: with the
-    default burn-in (24 x the longest span) the speculative chains meet the true ones; with a
-    1-2 tile burn-in they cannot, and the fix pass re-walks from the true chain values."""
+    default burn-in (6 x the longest span, the chains starting from the weighted-sum estimate)
+    the speculative chains meet the true ones; with a 1-2 tile burn-in the lanes' trade states
+    (and the longest span's chain) mostly do not, and the fix pass re-walks from the true values."""
     grid = D.Grid.ema_ols([10, 60, 390], [15, 120, 780], band_bps=20)
     cols = [F.gen(0x5EED, 60 + i, 40000, 1) for i in range(3)]
     ref, used1, _ = _run_grid(grid, cols, 1)
@@ -141,8 +142,9 @@ def test_ema_split_many_param_blocks(segments, burn):
     parameters span several blockIdx.y blocks that share the per-(segment, symbol) chain record:
     with a burn-in too short for the chains to meet, the fix pass must re-walk every y-block of
     a boundary (a fix pass that rewrote the shared start record would let later y-blocks keep
-    results built on the wrong chain)."""
-    spans = list(range(3, 3 + 2 * 30, 2))          # 30 spans
+    results built on the wrong chain). The 3,000-bar span keeps its chain from meeting the true
+    one within the short burn-in even from the weighted-sum start estimate."""
+    spans = list(range(3, 3 + 2 * 29, 2)) + [3000]  # 30 spans
     wins = list(range(4, 4 + 5 * 32, 5))           # 32 OLS windows -> 960 params
     grid = D.Grid.ema_ols(spans, wins, band_bps=15)
     assert grid.n_params > 896
