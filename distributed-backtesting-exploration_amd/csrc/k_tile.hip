@@ -345,7 +345,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     auto scan = [&](int T, int32_t c) {
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
-                                      dst + s * kDstLevels * kTile, cy);
+                                      dst + s * kDstLevels * kTile, cy, !BT_ABL(g, 512));
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (uint64_t)pre;
         const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end
@@ -363,8 +363,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         // the chain is the block's per-tile critical path (three dependent fp64 operations per
         // bar): issue it ahead of the other waves on its SIMD
         if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(3);
-        if (lane < nsp) {
-            if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
+        if (lane < nsp && !BT_ABL(g, 256)) {  // profiling: 256 drops the chain, 128 its math
+            if (BT_ABL(g, 128)) {
+#pragma unroll
+                for (int b = 0; b < kTile; ++b) E[b] = (double)__builtin_amdgcn_readlane(cl, b);
+            } else if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
 #pragma unroll
                 for (int b = 0; b < kTile; ++b) {
                     const double cd = (double)__builtin_amdgcn_readlane(cl, b);

@@ -19,7 +19,8 @@ struct TileCarry {
 // ql[64..127] (q2), and the disjoint sparse table D[6][64] of the close path. Returns the
 // inclusive prefix sum of closes up to this lane's bar (exact int64).
 __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane, int32_t* cT,
-                                             int64_t* ql, Agg* D, TileCarry& cy) {
+                                             int64_t* ql, Agg* D, TileCarry& cy,
+                                             bool with_dst = true) {
     const int t = t0 + lane;
     const bool valid = t < B;
     const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
@@ -33,7 +34,7 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     ql[kTile + lane] = wave_iscan_i64(q2);
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
-    dst_build(c, lane, D);
+    if (with_dst) dst_build(c, lane, D);  // (profiling ablation only: false skips the table)
     return pre;
 }
 
