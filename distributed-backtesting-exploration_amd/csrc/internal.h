@@ -12,8 +12,11 @@
 // release libbt.so BT_ABL is the constant false: no environment variable can change a result.
 #ifdef BT_PROFILING
 #define BT_ABL(g, bit) (((g).ablate & (bit)) != 0)
+// wave priority override (tuning aid): bit 20 set -> 2-bit field at `shift` replaces `dflt`
+#define BT_PRIO(g, shift, dflt) (BT_ABL(g, 1 << 20) ? (((g).ablate >> (shift)) & 3) : (dflt))
 #else
 #define BT_ABL(g, bit) false
+#define BT_PRIO(g, shift, dflt) (dflt)
 #endif
 
 namespace bt {

@@ -33,6 +33,24 @@ namespace bt {
 
 namespace {
 
+// wave priorities (s_setprio) of the pacing roles; BT_PRIO overrides them in the profiling build
+// (scripts/gpu_prio_sweep.sh). Round 3 sweep + release A/B: the accountant one level below the
+// finder, 7.23 -> 7.03 ms on config 4 at 500 symbols and 3.95 -> 3.83 at 250; the EMA chain at
+// the base priority (it raised the chain above the walk before), config 3 -0.5 to -1 %
+#ifndef BT_EMA_CHAIN_PRIO
+#define BT_EMA_CHAIN_PRIO 0
+#endif
+#ifndef BT_EMA_WALK_PRIO
+#define BT_EMA_WALK_PRIO 2
+#endif
+#ifndef BT_BOLL_WALK_PRIO
+#define BT_BOLL_WALK_PRIO 2
+#endif
+#ifndef BT_BOLL_ACCT_PRIO
+#define BT_BOLL_ACCT_PRIO 1
+#endif
+constexpr int kEmaChainPrio = BT_EMA_CHAIN_PRIO, kEmaWalkPrio = BT_EMA_WALK_PRIO;
+constexpr int kBollWalkPrio = BT_BOLL_WALK_PRIO, kBollAcctPrio = BT_BOLL_ACCT_PRIO;
 constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflict-free columns
 // Bollinger tile buffers: scanned (k+2), flagged (k+1), walked (k) and accounted (k-1, by the
 // accountant wave of a split walk)
@@ -360,9 +378,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         if (SEG && T < chain_T0) return;  // fix pass: bars before the segment are not needed
         const int t1 = T * kTile;
         double* E = ebuf + (T & 1) * estage + lane * kEStride;
-        // the chain is the block's per-tile critical path (three dependent fp64 operations per
-        // bar): issue it ahead of the other waves on its SIMD
-        if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(3);
+        // three dependent fp64 operations per bar; raising its priority over the walk no longer
+        // pays (the walk, tasks, scan and chain all set the tile together: DESIGN.md §4.2)
+        if (!BT_ABL(g, 32)) set_prio(BT_PRIO(g, 16, kEmaChainPrio));
         if (lane < nsp && !BT_ABL(g, 256)) {  // profiling: 256 drops the chain, 128 its math
             if (BT_ABL(g, 128)) {
 #pragma unroll
@@ -485,7 +503,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             seg_reset_sums(a);
         }
         if (active && k >= T_walk && !BT_ABL(g, 8)) {
-            __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
+            set_prio(BT_PRIO(g, 18, kEmaWalkPrio));  // the walk is the per-tile critical path
             const int s = k % kTileStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
@@ -1141,7 +1159,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             seg_reset_sums(a);
         }
         if (walks && k >= T_walk && k < T_end && !BT_ABL(g, 8)) {
-            __builtin_amdgcn_s_setprio(2);  // the walk is the per-tile critical path
+            set_prio(BT_PRIO(g, 16, kBollWalkPrio));  // the walk is the per-tile critical path
             const int s = k % kBollStages;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
@@ -1310,7 +1328,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         if (accountant && active && ka >= T_walk && ka < T_end && !BT_ABL(g, 8)) {
             // accountant: the finder's records of tile ka, in order (the tile's buffers stay
             // until step ka + 2: four stages, levels in three)
-            __builtin_amdgcn_s_setprio(2);
+            set_prio(BT_PRIO(g, 18, kBollAcctPrio));
             const int s = ka % kBollStages, ta = ka * kTile;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;

@@ -6,6 +6,17 @@
 
 namespace bt {
 
+// s_setprio takes an immediate: a wave-uniform priority through a scalar switch (folds to one
+// instruction for a constant)
+__device__ __forceinline__ void set_prio(int p) {
+    switch (p) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 constexpr int kTileStages = 3;  // tile buffers in flight: scanned (k+2), flagged (k+1), walked (k)
 
 

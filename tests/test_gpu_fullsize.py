@@ -1,7 +1,9 @@
 """BASELINE configs 3, 4 and 5 at their full per-GPU shard sizes on the GPU engine: sampled
-symbols bit-exact against the C oracle, plus size-independent properties over every lane
+symbols (24 of 500 for configs 3-4, 16 of 1,250 for config 5, every parameter) bit-exact against
+the C oracle, plus size-independent properties over every lane
 (counter totals, per-lane invariants, the exact top-k order over all results, and results that
 do not depend on which other symbols share the batch)."""
+import os
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -16,16 +18,30 @@ pytestmark = pytest.mark.gpu
 SEED = 0x5EED
 
 
-def _oracle_rows(strategy, grid, sym, bars, freq, ann):
-    o, h, lo, c = F.gen(SEED, sym, bars, freq)[:4]
+def _threads():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8
+    return max(1, min(16, aff))
 
-    def one(p):
-        kw = grid.param(p)
-        if strategy == "ema_ols":
-            return F.ema_ols(c, kw["n"], kw["w"], kw["band_bps"], ann)[0]
-        return F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], ann)[0]
+
+def _sample(S, n, seed):
+    """n symbols of a shard of S: both ends and seeded random ones in between."""
+    rng = np.random.default_rng(seed)
+    mid = rng.choice(np.arange(1, S - 1), n - 2, replace=False)
+    return sorted({0, S - 1, *(int(x) for x in mid)})
+
+
+def _oracle_grid(strategy, grid, syms, bars, ann):
+    """Every parameter of the sampled symbols on the oracle's pthread pool (one task per symbol)."""
     with ThreadPoolExecutor(8) as ex:
-        return list(ex.map(one, range(grid.n_params)))
+        cols = list(ex.map(lambda s: F.gen(SEED, s, bars, 1), syms))
+    closes = np.stack([c[3] for c in cols])
+    if strategy == "ema_ols":
+        return F.ema_grid_mt(closes, grid.axes[0], grid.axes[1], grid.band_bps, ann, _threads())
+    if strategy == "boll":
+        return F.boll_grid_mt(np.stack([c[1] for c in cols]), np.stack([c[2] for c in cols]), closes,
+                              grid.axes[0], grid.axes[1], grid.k_den, grid.axes[2], grid.axes[3],
+                              ann, _threads())
+    return F.sma_grid_mt(closes, np.asarray(grid.axes[0]), np.asarray(grid.axes[1]), ann, _threads())
 
 
 def _properties(allr, st, top, S, bars, P, k):
@@ -50,10 +66,11 @@ def test_config34_full_shard(config):
         e.run()
         allr, st, top = e.summaries(), e.stats(), e.read_topk()
     _properties(allr, st, top, S, bars, P, k)
-    for s in (0, 137, 499):
-        orc = _oracle_rows(strategy, grid, s, bars, 1, 98280)
+    sample = sorted(set(_sample(S, 24, config)) | {137})
+    orc = _oracle_grid(strategy, grid, sample, bars, 98280)
+    for i, s in enumerate(sample):
         for p in range(P):
-            compare_summary(allr[s, p], orc[p], f"config {config} sym {s} param {grid.param(p)}")
+            compare_summary(allr[s, p], orc[i, p], f"config {config} sym {s} param {grid.param(p)}")
     # batch independence: the same symbols alone give the same bits
     with D.Engine(grid) as e:
         e.load_synthetic(SEED, 137, 1, bars, D.BT_MINUTE)
@@ -75,9 +92,8 @@ def test_config5_full_shard():
     top_local = top.copy()
     top_local["sym"] -= 3750
     _properties(allr, st, top_local, S, bars, P, k)
-    sample = [0, 1249]
-    closes = np.stack([F.gen(SEED, 3750 + s, bars, 1)[3] for s in sample])
-    orc = F.sma_grid_mt(closes, np.asarray(grid.axes[0]), np.asarray(grid.axes[1]), 98280, 8)
+    sample = _sample(S, 16, 5)
+    orc = _oracle_grid("sma", grid, [3750 + s for s in sample], bars, 98280)
     for i, s in enumerate(sample):
         for p in range(P):
             compare_summary(allr[s, p], orc[i, p], f"config 5 sym {3750 + s} param {p}")
