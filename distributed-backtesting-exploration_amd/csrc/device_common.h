@@ -98,6 +98,17 @@ __device__ __forceinline__ int64_t wave_iscan_i64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Wave64 inclusive scan of uint32 (same DPP steps as wave_iscan_i64); lane 63 holds the total.
+__device__ __forceinline__ uint32_t wave_iscan_u32(uint32_t x) {
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 // ---- cross-lane moves without LDS (DPP / readlane; ds_bpermute costs an LDS round trip)
 // DPP controls: quad_perm [p0 p1 p2 p3] = p0 | p1 << 2 | p2 << 4 | p3 << 6; row_shl:d = 0x100 + d;
 // row_mirror 0x140; row_half_mirror 0x141 (lane i <-> 7 - i in each 8); row_newbcast:k = 0x150 + k

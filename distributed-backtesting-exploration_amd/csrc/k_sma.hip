@@ -37,7 +37,7 @@ constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
 
 struct SmaLds {                       // byte offsets into dynamic LDS
-    size_t ring, keys, invw, win, dst, ct, ql, ctr, total;
+    size_t ring, keys, invw, win, dst, ct, ql, nar, ctr, total;
 };
 
 __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
@@ -52,6 +52,7 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
+    L.nar = take((size_t)kStages * 4);    // per tile stage: accounts fit int32 (SmaAcct)
     L.ctr = take(4);
     L.total = o;
     return L;
@@ -61,6 +62,7 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
 struct ScanCarry {
     int64_t P;          // sum of closes before the tile
     int32_t prevc;      // close of the bar before the tile
+    uint64_t tv;        // total variation of the closes up to the tile (SmaAcct narrow tiles)
 };
 
 __device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, int B, int t) {
@@ -72,7 +74,8 @@ __device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, 
 // (prefix ring, closes, return prefixes) on the last wave and stage_dst (the drawdown table)
 // on the one before it, each from its own copy of the tile's closes.
 __device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, int R, double* ring,
-                                           int32_t* cT, int64_t* ql, ScanCarry& cy) {
+                                           int32_t* cT, int64_t* ql, int32_t* narrow,
+                                           ScanCarry& cy) {
     const int t = t0 + lane;
     const bool valid = t < B;
     // previous bar's close: DPP wave_shr:1, lane 0 takes the carry
@@ -82,9 +85,19 @@ __device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, i
     ring[(t + 1) & (R - 1)] = (double)(cy.P + inc);
     cT[lane] = c;
     int64_t q = 0, q2 = 0;
-    if (valid && t >= 1) fixed_ret(c, cp, q, q2);
+    uint32_t dv = 0;  // |c_t - c_(t-1)| (prices in [1, 2^31): the difference fits int32)
+    if (valid && t >= 1) {
+        fixed_ret(c, cp, q, q2);
+        dv = (uint32_t)abs(c - cp);
+    }
     ql[lane] = wave_iscan_i64(q);              // in-tile prefix: |.| <= 64 * 2^56 < 2^63
     ql[kTile + lane] = wave_iscan_i64(q2);
+    // the tile's total variation: a sum of 64 terms clamped to 2^25 fits uint32, and a clamped
+    // term alone puts TV past the narrow bound
+    const bool big = __ballot(dv >= (1u << 25)) != 0;
+    const uint32_t tvt = __builtin_amdgcn_readlane(wave_iscan_u32(min(dv, 1u << 25)), 63);
+    cy.tv += big ? (1ULL << 40) : (uint64_t)tvt;
+    if (lane == 0) *narrow = cy.tv < (1ULL << 30);
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
 }
@@ -204,9 +217,16 @@ __device__ __forceinline__ uint64_t eq_word(const int32_t* k1, const int32_t* k2
 //    each tile's true total is a masked sum of <= 64 q's, |.| < 2^63), folded into int128 at
 //    the tile end: entry at bar b adds -side*QL[b], exit adds +side*QL[b], an open position
 //    at the tile end adds +side*QL[63].
+//  * narrow tiles: every quantity the drawdown recursion touches (gap, mdd, a trade's lo, hi,
+//    path and pnl, the realized sum) is a difference of equity or price values at two bars, so
+//    its magnitude is at most the total variation TV = sum |c_t - c_(t-1)| of the closes so far,
+//    and gap - lo, max(gap, hi) - pnl at most 2 TV. While TV (through the tile's last bar) is
+//    below 2^30, the walk keeps gap / mdd / realized pnl in int32 (g32, m32, r32), exactly; at
+//    the first wider tile they move into the int64 fields for good.
 struct SmaAcct {
     int32_t pos, e, ce, sb, ntr, e0;     // sb: in-tile bar where the open trade's path resumes;
                                          // e0: first entry bar
+    int32_t g32, m32, r32;               // narrow tiles: gap, mdd, realized pnl
     int64_t R, gap, mdd;
     uint64_t ps1, ps2, h;
     i128 s1, s2;
@@ -228,7 +248,7 @@ struct SmaAcct {
 // MERGE = false: the trade opened in this tile (a.agg is the identity), so seg is its whole path.
 // SEG: a close of the carried trade (only possible with MERGE: the first close of a tile) is
 // recorded for the combine pass instead of accounted.
-template <bool PARITY, bool MERGE = true, bool SEG = false>
+template <bool PARITY, bool MERGE = true, bool SEG = false, bool NARROW = false>
 __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int32_t cx,
                                           bt_trade* tr, int cap) {
     const Agg st = MERGE ? agg_merge(a.agg, seg) : seg;   // seg: closes [sb, b] of this tile
@@ -251,11 +271,17 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int
         a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
         a.A = A0 - pnl;
         a.Bq = max(B0, (int64_t)hi) - pnl;
+    } else if (NARROW) {  // |.| <= 2 TV < 2^31 (SmaAcct)
+        a.m32 = max(a.m32, max(a.g32 - lo, path));
+        a.g32 = max(a.g32, hi) - pnl;
     } else {
         a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
         a.gap = max(a.gap, (int64_t)hi) - pnl;
     }
-    a.R += pnl;
+    if (NARROW)
+        a.r32 += pnl;
+    else
+        a.R += pnl;
     const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
                        ((uint64_t)lg << 62);
     a.h += trade_mix(w);
@@ -285,7 +311,7 @@ __device__ __forceinline__ void sma_open(SmaAcct& a, int b, int t, int32_t cx, i
 // closing trade may carry a path from earlier tiles (a.agg); every later reversal of the tile
 // closes a trade opened at the previous flip, so it skips the merge and leaves a.agg alone
 // (already the identity).
-template <bool PARITY, bool ONE_TRIP, bool FIRST, bool SEG>
+template <bool PARITY, bool ONE_TRIP, bool FIRST, bool SEG, bool NARROW>
 __device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& alt, int t0,
                                             const int32_t* cT, const int64_t* ql, const Agg* D,
                                             bt_trade* tr, int cap) {
@@ -313,14 +339,14 @@ __device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& a
         qb = (uint64_t)ql[b];
     }
     alt = qb - alt;
-    sma_close<PARITY, FIRST, SEG>(a, seg, t0 + b, cx, tr, cap);
+    sma_close<PARITY, FIRST, SEG, NARROW>(a, seg, t0 + b, cx, tr, cap);
     sma_open<FIRST>(a, b, t0 + b, cx, -a.pos);
 }
 
 // The tile's flips F (bar order). Sharpe partials: a close adds +pos * QL[b], an open subtracts
 // np * QL[b] (a reversal adds 2 pos QL[b]); the squared sum changes only on the first entry
 // (-Q2L[b]) and the forced exit (+Q2L[b]).
-template <bool PARITY, bool ONE_TRIP, bool SEG>
+template <bool PARITY, bool ONE_TRIP, bool SEG, bool NARROW>
 __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl, uint64_t LONG,
                                           const int32_t* cT, const int64_t* ql, const Agg* D,
                                           bt_trade* tr, int cap) {
@@ -340,13 +366,13 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
     // p_k = (-1)^(k-1) p_1 and adds 2 p_k QL[b_k]: an alternating sum, carried as
     // alt_k = QL[b_k] - alt_(k-1), so that sum = 2 p_n alt_n = -2 pos alt after the loop
     uint64_t alt = 0;
-    if (F) sma_reverse<PARITY, ONE_TRIP, true, SEG>(a, F, alt, t0, cT, ql, D, tr, cap);
-    while (F) sma_reverse<PARITY, ONE_TRIP, false, SEG>(a, F, alt, t0, cT, ql, D, tr, cap);
+    if (F) sma_reverse<PARITY, ONE_TRIP, true, SEG, NARROW>(a, F, alt, t0, cT, ql, D, tr, cap);
+    while (F) sma_reverse<PARITY, ONE_TRIP, false, SEG, NARROW>(a, F, alt, t0, cT, ql, D, tr, cap);
     a.ps1 += a.pos > 0 ? (uint64_t)0 - (alt << 1) : alt << 1;
     if (FX) {  // flat after bar B-1 (only set when a position is open before it)
         const int b = bl;
         const uint64_t qx = (uint64_t)ql[b];
-        sma_close<PARITY, true, SEG>(a, dst_query_bf(D, a.sb, b), t0 + b, cT[b], tr, cap);
+        sma_close<PARITY, true, SEG, NARROW>(a, dst_query_bf(D, a.sb, b), t0 + b, cT[b], tr, cap);
         a.ps1 += a.pos > 0 ? qx : (uint64_t)0 - qx;
         a.ps2 += (uint64_t)ql[kTile + b];
         a.pos = 0;
@@ -376,6 +402,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     Agg* dst = reinterpret_cast<Agg*>(smem + LL.dst);
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
+    int32_t* nars = reinterpret_cast<int32_t*>(smem + LL.nar);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x;
@@ -461,12 +488,12 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         cpre = load_close(crow, B, b0 + 2 * kTile + lane);
         const int s0 = T_walk % kStages, s1 = (T_walk + 1) % kStages;
         if (T_walk < T_end) {
-            if (helper) stage_ring(c0, B, b0, lane, R, ring, cts + s0 * kTile, qls + s0 * 2 * kTile, cy);
+            if (helper) stage_ring(c0, B, b0, lane, R, ring, cts + s0 * kTile, qls + s0 * 2 * kTile, nars + s0, cy);
             if (dstw || dsth) stage_dst(c0, lane, dst + s0 * kDstLevels * kTile);
         }
         __syncthreads();
         if (T_walk + 1 < T_end) {
-            if (helper) stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, cy);
+            if (helper) stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, nars + s1, cy);
             if (dstw || dsth) stage_dst(c1, lane, dst + s1 * kDstLevels * kTile);
         }
     } else {
@@ -479,6 +506,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
 
     SmaAcct a;
     a.pos = a.e = a.ce = a.sb = a.ntr = a.e0 = 0;
+    a.g32 = a.m32 = a.r32 = 0;
     a.R = a.gap = a.mdd = 0;
     a.ps1 = a.ps2 = 0;
     a.h = 0;
@@ -527,144 +555,165 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     }
     if (stamps) st_prev = __builtin_amdgcn_s_memtime();
 
-    for (int k = T_walk; k < T_end; ++k) {
-        const int t0 = k * kTile;
-        // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
-        // (tile k+1) on every wave, balanced dynamically
-        if ((helper || dstw) && k + 2 < T_end && !BT_ABL(g, 1)) {
-            // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
-            if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
-            const int s = (k + 2) % kStages;
-            if (helper)
-                stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
-                           qls + s * 2 * kTile, cy);
-            if (dstw || dsth) stage_dst(cpre, lane, dst + s * kDstLevels * kTile);
-            cpre = load_close(crow, B, t0 + 3 * kTile + lane);
-            __builtin_amdgcn_s_setprio(0);
+    // One tile (interval k of the pipeline). NARROW: the accounts run in int32 (SmaAcct) — the
+    // tiles of a symbol whose closes' total variation through the tile end is below 2^30, a
+    // prefix of its tiles (TV only grows): a loop over them, then a loop over the rest with
+    // int64 accounts, so each walk keeps its own registers.
+    auto tile_step = [&](auto narrow_tag, const int k) __attribute__((always_inline)) {
+        constexpr bool NARROW = decltype(narrow_tag)::value;
+            const int t0 = k * kTile;
+            // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
+            // (tile k+1) on every wave, balanced dynamically
+            if ((helper || dstw) && k + 2 < T_end && !BT_ABL(g, 1)) {
+                // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
+                if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
+                const int s = (k + 2) % kStages;
+                if (helper)
+                    stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+                               qls + s * 2 * kTile, nars + s, cy);
+                if (dstw || dsth) stage_dst(cpre, lane, dst + s * kDstLevels * kTile);
+                cpre = load_close(crow, B, t0 + 3 * kTile + lane);
+                __builtin_amdgcn_s_setprio(0);
+            }
+            BT_STAMP(0)
+            // ---- stage 3 (tile k)
+            if (SEG && active && k == T_acct && k != T_walk) enter_acct();
+            if (active) {
+                // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
+                // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
+                // blocks are ~1 % slower with it)
+                if (ONE_TRIP) __builtin_amdgcn_s_setprio(1);
+                const int s = k % kStages;
+                const int32_t* cT = cts + s * kTile;
+                const int64_t* ql = qls + s * 2 * kTile;
+                const Agg* D = dst + s * kDstLevels * kTile;
+                const int32_t* K = keys + (k & 1) * nwp * kKS;
+                const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
+                const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
+                uint32_t l0 = 0, l1 = 0, z = ~0u;
+                if (!BT_ABL(g, 4)) {
+                    // all reads at immediate offsets from one address per row
+    #pragma unroll
+                    for (int v = 0; v < 16; ++v) {
+                        if (v < 8) cmp4(l0, z, k1[v], k2[v]);
+                        else cmp4(l1, z, k1[v], k2[v]);
+                        // keep the schedule to two int4 pairs in flight (VGPR budget)
+                        if (v & 1) __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+                BT_STAMP(2)
+                uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
+                const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
+                const int wb = warm - t0;
+                const int bl = B - 1 - t0;       // forced exit: flat after bar B-1
+                uint64_t LONG, F;
+                if (z != 0 && wb <= 0 && lastdec >= 63) {
+                    // every bar decides and no keys are equal: the position after bar b is simply
+                    // long iff fast > slow (LONG = G = ~L), and the flips are its changes
+                    LONG = ~L;
+                    F = (LONG ^ ((LONG << 1) | (uint64_t)(a.pos == 1))) | (uint64_t)(a.pos == 0);
+                } else {
+                    uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
+                    vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
+                    uint64_t G, T = 0;
+                    if (z != 0) {
+                        G = ~L & vm;
+                    } else {  // some bar has equal floor keys: settle those exactly
+                        const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
+                        G = ~(L | E) & vm;
+                        T = E & vm;
+                    }
+                    L &= vm;
+                    while (T) {
+                        const int b = __builtin_ctzll(T);
+                        T &= T - 1;
+                        const int t = t0 + b;
+                        // window sums are exact in the ring (< 2^53) and < 2^31 w; F s and L f
+                        // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
+                        // so the tie is settled in int64 for every grid the engine accepts
+                        const double top = ring[(t + 1) & (R - 1)];
+                        const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
+                        const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
+                        G |= (uint64_t)(Fs > Lf) << b;
+                        L |= (uint64_t)(Fs < Lf) << b;
+                    }
+                    // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
+                    uint64_t SHORT;
+                    {
+                        const uint64_t A = ~L;
+                        const uint64_t s1 = A + G;
+                        uint64_t cout = s1 < A;
+                        const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
+                        cout |= sum < s1;
+                        LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
+                    }
+                    {
+                        const uint64_t A = ~G;
+                        const uint64_t s1 = A + L;
+                        uint64_t cout = s1 < A;
+                        const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
+                        cout |= sum < s1;
+                        SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
+                    }
+                    if (bl < 64) {
+                        const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
+                        LONG &= keep;
+                        SHORT &= keep;
+                    }
+                    const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
+                    const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
+                    F = (LONG ^ pL) | (SHORT ^ pS);
+                }
+                BT_STAMP(3)
+                uint64_t Fw = F;
+                if (BT_ABL(g, 8)) {  // profiling: drop the trade events (keep F live)
+                    asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
+                    Fw = 0;
+                }
+                sma_flips<PARITY, ONE_TRIP, SEG, NARROW>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
+                BT_STAMP(4)
+                if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
+                    a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
+                    a.sb = 0;
+                    const uint64_t q63 = (uint64_t)ql[kTile - 1];
+                    a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
+                    a.ps2 += (uint64_t)ql[2 * kTile - 1];
+                }
+                // fold the return partials into int128 every second tile (and at the last): over
+                // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
+                // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
+                // zero price), so the uint64 partials are exact as int64
+                if ((k & 1) || k + 1 == T_end) {
+                    a.s1 += (i128)(int64_t)a.ps1;
+                    a.s2 += (i128)(int64_t)a.ps2;
+                    a.ps1 = a.ps2 = 0;
+                }
+                BT_STAMP(5)
+                if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
+            }
+            if (k + 1 < T_end && !BT_ABL(g, 2))
+                stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
+                           ctr, (uint32_t)(k + 1), nwaves, lane);
+            BT_STAMP(1)
+            __syncthreads();
+            BT_STAMP(6)
+    };
+    int k = T_walk;
+    if (!SEG && k < T_end) {
+        bool nar = __builtin_amdgcn_readfirstlane(nars[k % kStages]) != 0;
+        while (nar) {
+            // the flag of tile k + 1: written by stage 1 two intervals ago, rewritten (tile k + 4)
+            // only in interval k + 2
+            const int32_t nn = k + 1 < T_end ? nars[(k + 1) % kStages] : 0;
+            tile_step(std::true_type{}, k);
+            nar = __builtin_amdgcn_readfirstlane(nn) != 0;
+            ++k;
         }
-        BT_STAMP(0)
-        // ---- stage 3 (tile k)
-        if (SEG && active && k == T_acct && k != T_walk) enter_acct();
-        if (active) {
-            // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
-            // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
-            // blocks are ~1 % slower with it)
-            if (ONE_TRIP) __builtin_amdgcn_s_setprio(1);
-            const int s = k % kStages;
-            const int32_t* cT = cts + s * kTile;
-            const int64_t* ql = qls + s * 2 * kTile;
-            const Agg* D = dst + s * kDstLevels * kTile;
-            const int32_t* K = keys + (k & 1) * nwp * kKS;
-            const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
-            const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
-            uint32_t l0 = 0, l1 = 0, z = ~0u;
-            if (!BT_ABL(g, 4)) {
-                // all reads at immediate offsets from one address per row
-#pragma unroll
-                for (int v = 0; v < 16; ++v) {
-                    if (v < 8) cmp4(l0, z, k1[v], k2[v]);
-                    else cmp4(l1, z, k1[v], k2[v]);
-                    // keep the schedule to two int4 pairs in flight (VGPR budget)
-                    if (v & 1) __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            BT_STAMP(2)
-            uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
-            const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
-            const int wb = warm - t0;
-            const int bl = B - 1 - t0;       // forced exit: flat after bar B-1
-            uint64_t LONG, F;
-            if (z != 0 && wb <= 0 && lastdec >= 63) {
-                // every bar decides and no keys are equal: the position after bar b is simply
-                // long iff fast > slow (LONG = G = ~L), and the flips are its changes
-                LONG = ~L;
-                F = (LONG ^ ((LONG << 1) | (uint64_t)(a.pos == 1))) | (uint64_t)(a.pos == 0);
-            } else {
-                uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
-                vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
-                uint64_t G, T = 0;
-                if (z != 0) {
-                    G = ~L & vm;
-                } else {  // some bar has equal floor keys: settle those exactly
-                    const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
-                    G = ~(L | E) & vm;
-                    T = E & vm;
-                }
-                L &= vm;
-                while (T) {
-                    const int b = __builtin_ctzll(T);
-                    T &= T - 1;
-                    const int t = t0 + b;
-                    // window sums are exact in the ring (< 2^53) and < 2^31 w; F s and L f
-                    // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
-                    // so the tie is settled in int64 for every grid the engine accepts
-                    const double top = ring[(t + 1) & (R - 1)];
-                    const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
-                    const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
-                    G |= (uint64_t)(Fs > Lf) << b;
-                    L |= (uint64_t)(Fs < Lf) << b;
-                }
-                // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
-                uint64_t SHORT;
-                {
-                    const uint64_t A = ~L;
-                    const uint64_t s1 = A + G;
-                    uint64_t cout = s1 < A;
-                    const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
-                    cout |= sum < s1;
-                    LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
-                }
-                {
-                    const uint64_t A = ~G;
-                    const uint64_t s1 = A + L;
-                    uint64_t cout = s1 < A;
-                    const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
-                    cout |= sum < s1;
-                    SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
-                }
-                if (bl < 64) {
-                    const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
-                    LONG &= keep;
-                    SHORT &= keep;
-                }
-                const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
-                const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
-                F = (LONG ^ pL) | (SHORT ^ pS);
-            }
-            BT_STAMP(3)
-            uint64_t Fw = F;
-            if (BT_ABL(g, 8)) {  // profiling: drop the trade events (keep F live)
-                asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
-                Fw = 0;
-            }
-            sma_flips<PARITY, ONE_TRIP, SEG>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
-            BT_STAMP(4)
-            if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
-                a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
-                a.sb = 0;
-                const uint64_t q63 = (uint64_t)ql[kTile - 1];
-                a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
-                a.ps2 += (uint64_t)ql[2 * kTile - 1];
-            }
-            // fold the return partials into int128 every second tile (and at the last): over
-            // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
-            // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
-            // zero price), so the uint64 partials are exact as int64
-            if ((k & 1) || k + 1 == T_end) {
-                a.s1 += (i128)(int64_t)a.ps1;
-                a.s2 += (i128)(int64_t)a.ps2;
-                a.ps1 = a.ps2 = 0;
-            }
-            BT_STAMP(5)
-            if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
-        }
-        if (k + 1 < T_end && !BT_ABL(g, 2))
-            stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
-                       ctr, (uint32_t)(k + 1), nwaves, lane);
-        BT_STAMP(1)
-        __syncthreads();
-        BT_STAMP(6)
+        a.gap = (uint32_t)a.g32;  // >= 0
+        a.mdd = (uint32_t)a.m32;
+        a.R = a.r32;
     }
+    for (; k < T_end; ++k) tile_step(std::false_type{}, k);
 #undef BT_STAMP
     if (stamps && lane == 0) {
         unsigned long long* d = out.dbg + (helper ? 8 : 0);

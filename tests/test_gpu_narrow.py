@@ -1,0 +1,84 @@
+"""GPU parity of the SMA kernel's narrow accounts (k_sma.hip SmaAcct): while the total variation
+TV = sum |c_t - c_(t-1)| of a symbol's closes stays below 2^30 the walk keeps gap, mdd and the
+realized pnl in int32, then moves them into int64 for the rest of the series. These series
+cross the bound at different tiles (and bars inside a tile), one by a single jump of 2^25 ticks
+or more (the scan's clamped-term branch), one never crosses and one is wide from its first tile;
+every summary field and every trade must equal the C oracle's, in the release and the parity
+instantiations."""
+import numpy as np
+import pytest
+
+import dbx_amd as D
+from helpers import compare_summary, compare_trades, oracle_row
+
+CAP = 4096
+BARS = 2520
+LO, HI = 10_000, 2**31 - 2**20
+
+
+def _walk(rng, c0, step, bars=BARS, lo=LO):
+    c = np.empty(bars, np.int64)
+    c[0] = c0
+    d = rng.integers(-step, step + 1, bars)
+    for t in range(1, bars):
+        c[t] = min(max(c[t - 1] + d[t], lo), HI)
+    return c
+
+
+def _series():
+    rng = np.random.default_rng(20261017)
+    out = []
+    for step in (1 << 20, 3 << 19, 1 << 21, 1 << 22, 1 << 23):  # TV crosses 2^30 late ... early
+        out.append(_walk(rng, 1 << 28, step))
+    c = _walk(rng, 1 << 27, 1 << 15)                            # a jump of 2^26 at bar 1,000
+    c[1000:] = np.clip(c[1000:] + (1 << 26), LO, HI)
+    out.append(c)
+    out.append(_walk(rng, 5_000_000, 20_000))                   # TV ~ 2.5e7: narrow throughout
+    out.append(_walk(rng, 1 << 30, 1 << 26, lo=1 << 28))       # steps past 2^25: wide at once
+    return [x.astype(np.int32) for x in out]
+
+
+def _first_wide_tile(c):
+    """The kernel's rule (k_sma.hip stage_ring): per 64-bar tile TV grows by the clamped sum of
+    |c_t - c_(t-1)|, or by 2^40 if one term reaches 2^25; tiles are narrow while TV < 2^30."""
+    d = np.zeros(len(c), np.int64)
+    d[1:] = np.abs(np.diff(c.astype(np.int64)))
+    tv = 0
+    for k in range((len(c) + 63) // 64):
+        x = d[64 * k:64 * k + 64]
+        tv += (1 << 40) if (x >= (1 << 25)).any() else int(np.minimum(x, 1 << 25).sum())
+        if tv >= (1 << 30):
+            return k
+    return None
+
+
+def test_series_cross_the_narrow_bound_where_intended():
+    ks = [_first_wide_tile(c) for c in _series()]
+    assert all(k is not None and 0 < k < BARS // 64 - 1 for k in ks[:6]), ks
+    assert len(set(ks[:6])) == 6, ks          # six different crossing tiles
+    assert ks[5] == 1000 // 64, ks            # the jump's tile (clamped-term branch)
+    assert ks[6] is None and ks[7] == 0, ks
+    for c in _series():  # valid input (docs/oracle_spec.md: |ret| <= 1, i.e. c_t <= 2 c_(t-1))
+        c = c.astype(np.int64)
+        assert c.min() >= 1 and (c[1:] <= 2 * c[:-1]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parity", [False, True])
+def test_sma_narrow_to_wide_accounts_match_oracle(parity):
+    grid = D.config2_grid()
+    closes = _series()
+    kw = dict(parity=True, trade_cap=CAP) if parity else {}
+    with D.Engine(grid, **kw) as e:
+        e.load_ohlc(closes)
+        e.run()
+        got = e.summaries()
+        tr = e.trades() if parity else None
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("sma", grid, (cl, cl, cl, cl), 252, CAP if parity else 0)
+        big = max(int(o["mdd"]) for o in orc)
+        for p in range(grid.n_params):
+            where = f"series {s} (first wide tile {_first_wide_tile(cl)}, max mdd {big}) {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            if parity:
+                compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)

@@ -6,7 +6,7 @@ the kernels, read with the ROCm LLVM tools).
   first version, round 2), and it happens silently.
 * The tile kernels must keep <= 128 VGPRs: two 8-wave blocks per CU (config 4 at 500 symbols
   per GPU) need 4 waves per SIMD.
-Parity instantiations (trade lists, test path only: the SMA one spills 3 VGPRs at its 80-VGPR
+Parity instantiations (trade lists, test path only: the SMA ones spill a few VGPRs at their 80-VGPR
 budget) are exempt from the scratch and spill checks."""
 import os
 import re
