@@ -42,29 +42,38 @@ __device__ __forceinline__ Agg agg_merge(const Agg& a, const Agg& b) {
     return r;
 }
 
+// Rows of the table are stored in reverse level order (row 5 - m holds level m): the row of a
+// query (a, b) is then clz((a ^ b) | 1) - 26, one v_ffbh and no select, with a == b landing on
+// level 0 (the single bar).
+__device__ __forceinline__ int dst_row(int a, int b) {
+    return __builtin_clz((unsigned)(a ^ b) | 1u) - (32 - kDstLevels);
+}
+// The row's base (the constant offset folds into the table's scalar base address).
+__device__ __forceinline__ const Agg* dst_rowp(const Agg* D, int a, int b) {
+    return D - (32 - kDstLevels) * kTile + __builtin_clz((unsigned)(a ^ b) | 1u) * kTile;
+}
+
 // Aggregate of closes cT[a..b], 0 <= a <= b < kTile.
 __device__ __forceinline__ Agg dst_query(const Agg* D, const int32_t* cT, int a, int b) {
     if (a == b) return agg_one(cT[a]);
-    const int L = 31 - __builtin_clz((unsigned)(a ^ b));
-    return agg_merge(D[L * kTile + a], D[L * kTile + b]);
+    const int r = dst_row(a, b);
+    return agg_merge(D[r * kTile + a], D[r * kTile + b]);
 }
 
 // Branch-free form: for a == b level 0 holds the single bar (D[0][a] == one(c_a)), and
 // merging it with itself leaves max/min unchanged and gives drawdown/draw-up 0.
 __device__ __forceinline__ Agg dst_query_bf(const Agg* D, int a, int b) {
-    const unsigned x = (unsigned)(a ^ b);
-    const int L = x ? 31 - __builtin_clz(x) : 0;
-    return agg_merge(D[L * kTile + a], D[L * kTile + b]);
+    const Agg* Dr = dst_rowp(D, a, b);
+    return agg_merge(Dr[a], Dr[b]);
 }
 
 // dst_query_bf reading both 16-B entries whole (two ds_read_b128 in one round trip, kept live):
 // callers that need drawdown or draw-up by side then wait once instead of a second time in a
 // divergent branch.
 __device__ __forceinline__ Agg dst_query_w(const Agg* D, int a, int b) {
-    const unsigned x = (unsigned)(a ^ b);
-    const int L = x ? 31 - __builtin_clz(x) : 0;
-    const int4 u = *reinterpret_cast<const int4*>(D + L * kTile + a);
-    const int4 v = *reinterpret_cast<const int4*>(D + L * kTile + b);
+    const Agg* Dr = dst_rowp(D, a, b);
+    const int4 u = *reinterpret_cast<const int4*>(Dr + a);
+    const int4 v = *reinterpret_cast<const int4*>(Dr + b);
     asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
     return agg_merge(Agg{u.x, u.y, u.z, u.w}, Agg{v.x, v.y, v.z, v.w});
 }
@@ -163,14 +172,14 @@ __device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
 // first lane's suffix) into its prefix Pp; partners move by DPP / readlane, no LDS round trip.
 __device__ __forceinline__ void dst_build(int32_t c, int lane, Agg* D) {
     Agg S = agg_one(c), Pp = S;
-    D[lane] = S;
+    D[(kDstLevels - 1) * kTile + lane] = S;  // level 0: the last row (dst_row)
     auto level = [&](auto mtag) {
         constexpr int m = decltype(mtag)::value;
         const bool left = (lane & (1 << (m - 1))) == 0;
         const Agg part = dst_partner_agg<m>(agg_sel(left, S, Pp), lane);
         S = agg_sel(left, agg_merge(S, part), S);
         Pp = agg_sel(left, Pp, agg_merge(part, Pp));
-        D[m * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
+        D[(kDstLevels - 1 - m) * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);
     };
     level(std::integral_constant<int, 1>{});
     level(std::integral_constant<int, 2>{});

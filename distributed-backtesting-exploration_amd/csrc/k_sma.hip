@@ -324,9 +324,8 @@ __device__ __forceinline__ void sma_reverse(SmaAcct& a, uint64_t& F, uint64_t& a
         // all four LDS reads of the iteration issued before one wait: pays at low occupancy
         // (config 5's one 16-wave block per CU: 157.7 -> 152.1 ms), costs ~1 % at config 2's
         // six waves per SIMD, where the compiler's two round trips are hidden anyway
-        const unsigned xs = (unsigned)(a.sb ^ b);
-        const int lv = xs ? 31 - __builtin_clz(xs) : 0;
-        const Agg d1 = D[lv * kTile + a.sb], d2 = D[lv * kTile + b];
+        const Agg* Dr = dst_rowp(D, a.sb, b);
+        const Agg d1 = Dr[a.sb], d2 = Dr[b];
         cx = cT[b];
         qb = (uint64_t)ql[b];
         asm volatile("" ::"v"(d1.mx), "v"(d1.mn), "v"(d1.dd), "v"(d1.du), "v"(d2.mx),

@@ -39,7 +39,7 @@ int main() {
                 if (m == 0) e = one(h[i]);
                 else if ((i >> m) & 1) { e = one(h[start]); for (int j = start + 1; j <= i; ++j) e = mg(e, one(h[j])); }
                 else { e = one(h[i]); for (int j = i + 1; j < start + half; ++j) e = mg(e, one(h[j])); }
-                const Agg g = got[m * 64 + i];
+                const Agg g = got[(5 - m) * 64 + i];  // rows in reverse level order (dst_row)
                 if (g.mx != e.mx || g.mn != e.mn || g.dd != e.dd || g.du != e.du) {
                     if (bad++ < 20) printf("it %d level %d lane %d: got (%d %d %d %d) want (%d %d %d %d)\n", it, m, i, g.mx, g.mn, g.dd, g.du, e.mx, e.mn, e.dd, e.du);
                 }
