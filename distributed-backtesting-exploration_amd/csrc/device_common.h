@@ -158,8 +158,16 @@ __device__ __forceinline__ int32_t dst_partner(int32_t x, int lane) {
 }
 
 // The Agg of the level-M partner lane (dst_partner).
-template <int M>
+template <int M, bool LDSX = false>
 __device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
+    if constexpr (LDSX && M >= 3) {
+        // one ds_bpermute per field instead of 3-7 DPP / readlane / select VALU: for a table
+        // built as a task off the pipeline's critical path, issue slots count, not latency
+        constexpr int half = 1 << (M - 1), grp = 1 << M;
+        const int src = (lane & half) ? (lane & ~(grp - 1)) : (lane | (grp - 1));
+        return Agg{__builtin_amdgcn_ds_bpermute(src << 2, a.mx), __builtin_amdgcn_ds_bpermute(src << 2, a.mn),
+                   __builtin_amdgcn_ds_bpermute(src << 2, a.dd), __builtin_amdgcn_ds_bpermute(src << 2, a.du)};
+    }
     return Agg{dst_partner<M>(a.mx, lane), dst_partner<M>(a.mn, lane), dst_partner<M>(a.dd, lane),
                dst_partner<M>(a.du, lane)};
 }
@@ -170,13 +178,15 @@ __device__ __forceinline__ Agg dst_partner_agg(const Agg& a, int lane) {
 // Doubling: at level m a lane in the left half of its 2^m group merges the right half (exposed
 // as the group's last lane's prefix) into its suffix S, a right-half lane the left half (the
 // first lane's suffix) into its prefix Pp; partners move by DPP / readlane, no LDS round trip.
+template <bool LDSX = false>
 __device__ __forceinline__ void dst_build(int32_t c, int lane, Agg* D) {
+    if (LDSX) asm volatile("" : "+v"(lane));  // the partner addresses are not hoisted and kept live
     Agg S = agg_one(c), Pp = S;
     D[(kDstLevels - 1) * kTile + lane] = S;  // level 0: the last row (dst_row)
     auto level = [&](auto mtag) {
         constexpr int m = decltype(mtag)::value;
         const bool left = (lane & (1 << (m - 1))) == 0;
-        const Agg part = dst_partner_agg<m>(agg_sel(left, S, Pp), lane);
+        const Agg part = dst_partner_agg<m, LDSX>(agg_sel(left, S, Pp), lane);
         S = agg_sel(left, agg_merge(S, part), S);
         Pp = agg_sel(left, Pp, agg_merge(part, Pp));
         D[(kDstLevels - 1 - m) * kTile + lane] = agg_sel(((lane >> m) & 1) != 0, Pp, S);

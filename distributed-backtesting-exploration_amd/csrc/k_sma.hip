@@ -8,11 +8,13 @@
 // tile at a time, in a three-stage software pipeline with ONE workgroup barrier per tile:
 //   stage 1, tile k+2 (a dedicated helper wave): exact int64 prefix of close appended to a ring
 //            of doubles (exact below 2^53); fixed-point returns q, q2 (spec §3) and their
-//            in-tile int64 prefixes + int128 tile base; the tile's disjoint sparse table (DST) of
-//            the close path (max, min, drawdown, draw-up), built by log-doubling shuffles.
-//   stage 2, tile k+1 (all waves, helper included; lane = bar, window wave-uniform): int32 SMA
+//            in-tile int64 prefixes + int128 tile base; the closes' total variation (narrow
+//            accounts, SmaAcct).
+//   stage 2, tile k+1 (all waves, helper included, tasks grabbed from an LDS counter): the
+//            tile's disjoint sparse table (DST) of the close path (max, min, drawdown, draw-up),
+//            built by log-doubling shuffles, and (lane = bar, window wave-uniform) int32 SMA
 //            keys K[w][b] = floor(window_sum / w) for every window of the grid (one f64
-//            multiply + exact fix-up, no division).
+//            multiply, no division).
 //   stage 3, tile k (parameter waves, lane = (fast, slow) pair): per bar one subtract whose
 //            sign bit is shifted into the 64-bit word L (fast key < slow key), and a running
 //            unsigned min that detects equal keys; without equal keys G (fast > slow) = ~L.
@@ -33,7 +35,8 @@ namespace bt {
 namespace {
 
 constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned for b128 reads
-constexpr int kStages = 3;            // tile buffers in flight (cT, Q, DST)
+constexpr int kStages = 3;            // tile buffers in flight (cT, Q)
+constexpr int kDstStages = 2;         // drawdown tables: built in interval k - 1, read in k
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
 
 struct SmaLds {                       // byte offsets into dynamic LDS
@@ -49,7 +52,7 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     L.keys = take((size_t)2 * nwp * kKS * 4);
     L.invw = take((size_t)nwp * 8);
     L.win = take((size_t)nwp * 4);
-    L.dst = take((size_t)kStages * kDstLevels * kTile * sizeof(Agg));
+    L.dst = take((size_t)kDstStages * kDstLevels * kTile * sizeof(Agg));
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
     L.nar = take((size_t)kStages * 4);    // per tile stage: accounts fit int32 (SmaAcct)
@@ -62,7 +65,8 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
 struct ScanCarry {
     int64_t P;          // sum of closes before the tile
     int32_t prevc;      // close of the bar before the tile
-    uint64_t tv;        // total variation of the closes up to the tile (SmaAcct narrow tiles)
+    uint32_t tv;        // total variation of the closes up to the tile, saturated at 2^31
+                        // (SmaAcct narrow tiles)
 };
 
 __device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, int B, int t) {
@@ -70,9 +74,8 @@ __device__ __forceinline__ int32_t load_close(const int32_t* __restrict__ crow, 
 }
 
 // c = close of bar t0 + lane (0 past the end), loaded one tile ahead by the caller so the HBM
-// latency is off the pipeline's critical path. Stage 1 is split over two waves: stage_ring
-// (prefix ring, closes, return prefixes) on the last wave and stage_dst (the drawdown table)
-// on the one before it, each from its own copy of the tile's closes.
+// latency is off the pipeline's critical path. The tile's drawdown table is a stage-2 task
+// (stage_keys), built from the closes stored here.
 __device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, int R, double* ring,
                                            int32_t* cT, int64_t* ql, int32_t* narrow,
                                            ScanCarry& cy) {
@@ -96,14 +99,11 @@ __device__ __forceinline__ void stage_ring(int32_t c, int B, int t0, int lane, i
     // term alone puts TV past the narrow bound
     const bool big = __ballot(dv >= (1u << 25)) != 0;
     const uint32_t tvt = __builtin_amdgcn_readlane(wave_iscan_u32(min(dv, 1u << 25)), 63);
-    cy.tv += big ? (1ULL << 40) : (uint64_t)tvt;
-    if (lane == 0) *narrow = cy.tv < (1ULL << 30);
+    cy.tv = big ? (1u << 31) : min(cy.tv + tvt, 1u << 31);  // both terms < 2^31: no wrap
+    if (lane == 0) *narrow = cy.tv < (1u << 30);
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
 }
-
-// The tile's drawdown table (device_common.h dst_build), from this wave's copy of the closes.
-__device__ __forceinline__ void stage_dst(int32_t c, int lane, Agg* D) { dst_build(c, lane, D); }
 
 // Stage 2 for one tile: int32 floor keys for every window. lane = bar, so the window length
 // and its reciprocal are wave-uniform and the top of the ring is read once per tile.
@@ -135,20 +135,36 @@ __device__ __forceinline__ int32_t floor_key(double F, double iw) {
     return (int32_t)(F * iw);
 }
 
+// Counter values of one stage-2 round: the drawdown-table task, the key groups, and one failing
+// grab per wave.
+__host__ __device__ inline uint32_t key_round_len(int nwp, int nwaves) {
+    return (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + 1 + (uint32_t)nwaves);
+}
+
+// Stage 2 of round r (tile r): the tile's drawdown table (device_common.h dst_build) from the
+// closes stage 1 left in LDS (cTr), into Dr, as the round's first task, then the key groups.
+// The table is a task rather than a fixed role: on the half-empty seventh parameter wave of a
+// config-2 block it set the tile (that wave's compare and walk plus the table's DPP chain).
 __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nwp, int nf, int wmax, int R,
                                            const double* ring, const int32_t* win,
                                            const double* invw, int32_t* K, uint32_t* ctr,
-                                           uint32_t round, int nwaves, int lane) {
+                                           uint32_t round, int nwaves, int lane,
+                                           const int32_t* cTr, Agg* Dr) {
     const int t = t0 + lane;
     const double top = ring[(t + 1) & (R - 1)];
     // wave-uniform: every bar of the tile has a full window for every window length
     const bool full = t0 + 1 - wmax >= 0 && t0 + kTile <= B;
-    const uint32_t per = (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + nwaves);
-    const uint32_t base = round * per;
+    const uint32_t base = round * key_round_len(nwp, nwaves);
     uint32_t w = __builtin_amdgcn_readlane(grab_issue(ctr, lane), 0) - base;
 #pragma unroll 1
-    while (w < (uint32_t)nwp) {
+    while (w < (uint32_t)(nwp + kKeyGrab)) {
         const uint32_t vn = grab_issue(ctr, lane);  // next group, read at the end
+        if (w == 0) {
+            dst_build<true>(cTr[lane], lane, Dr);
+            w = __builtin_amdgcn_readlane(vn, 0) - base;
+            continue;
+        }
+        w -= kKeyGrab;
         // w is a multiple of kKeyGrab: the group's lengths and reciprocals are aligned 16-B
         // reads; rows nw..nwp-1 are padding (length 1) whose keys nobody reads
         int Wv[kKeyGrab];
@@ -223,13 +239,27 @@ __device__ __forceinline__ uint64_t eq_word(const int32_t* k1, const int32_t* k2
 //    and gap - lo, max(gap, hi) - pnl at most 2 TV. While TV (through the tile's last bar) is
 //    below 2^30, the walk keeps gap / mdd / realized pnl in int32 (g32, m32, r32), exactly; at
 //    the first wider tile they move into the int64 fields for good.
+// A 96-bit signed accumulator (two VGPRs fewer than int128): the Sharpe sums are bounded by
+// 2^22 bars x 2^56 < 2^78 (spec §3), and 2^95 leaves room to spare.
+struct I96 {
+    uint64_t lo;
+    int32_t hi;
+    __device__ __forceinline__ void clear() { lo = 0; hi = 0; }
+    __device__ __forceinline__ void add(int64_t x) {
+        const uint64_t n = lo + (uint64_t)x;
+        hi += (int32_t)(n < lo) - (int32_t)(x < 0);  // carry out of the low word, sign of x
+        lo = n;
+    }
+    __device__ __forceinline__ int64_t hi64() const { return (int64_t)hi; }
+};
+
 struct SmaAcct {
     int32_t pos, e, ce, sb, ntr, e0;     // sb: in-tile bar where the open trade's path resumes;
                                          // e0: first entry bar
     int32_t g32, m32, r32;               // narrow tiles: gap, mdd, realized pnl
     int64_t R, gap, mdd;
     uint64_t ps1, ps2, h;
-    i128 s1, s2;
+    I96 s1, s2;
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
     // bar segments (SEG) only: the drawdown as max-plus forms of the unknown entering gap and mdd
     // (tile_common.h TradeAcct), and the trade open at the segment start, whose entry lies in an
@@ -406,15 +436,11 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // the last wave runs stage 1; with `dedicated` it is a helper with no parameter lanes,
     // otherwise (a grid that fills all 16 waves of one block) it also walks 64 parameters
     const int nwaves = (int)blockDim.x >> 6;
     const bool helper = (tid >> 6) == nwaves - 1;
-    // the wave before it builds the drawdown tables (stage_dst); profiling bit 16 keeps both
-    // parts of stage 1 on the last wave
-    const bool split = !BT_ABL(g, 16);
-    const bool dstw = split && (tid >> 6) == nwaves - 2;
-    const bool dsth = helper && !split;
     const int nparam_threads = dedicated ? (int)blockDim.x - 64 : (int)blockDim.x;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars;
@@ -449,7 +475,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
 
     const int nwp = (nw + kKeyGrab - 1) / kKeyGrab * kKeyGrab;
-    const uint32_t key_round = (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + nwaves);
+    const uint32_t key_round = key_round_len(nwp, nwaves);
     for (int w = tid; w < nwp; w += blockDim.x) {
         const int W = w < nf ? g.a[w] : (w < nw ? g.b[w - nf] : 1);
         win[w] = W;
@@ -460,8 +486,9 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         *ctr = (uint32_t)T_walk * key_round;     // key rounds are numbered by tile
     }
     __syncthreads();
-    const int fw = win[kf], sw = win[ks];
-    const int warm = (fw > sw ? fw : sw) - 1;  // first decision bar of this lane
+    const int warm = max(win[kf], win[ks]) - 1;  // first decision bar of this lane
+    // both window lengths in one register (each < 2^16), for the rare exact tie settle
+    const uint32_t fsw = (uint32_t)win[kf] | ((uint32_t)win[ks] << 16);
 
     ScanCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     // SEG lookback: the prefix ring over the windows before the first walked bar (the next tile's
@@ -481,26 +508,22 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     // prologue: stage 1 for the first two walked tiles; stage 2 for the first. The helper keeps
     // the closes of the tile after next in flight (cpre) across the barrier.
     int32_t cpre = 0;
-    if (helper || dstw) {
+    if (helper) {
         const int b0 = T_walk * kTile;
         const int32_t c0 = load_close(crow, B, b0 + lane), c1 = load_close(crow, B, b0 + kTile + lane);
         cpre = load_close(crow, B, b0 + 2 * kTile + lane);
         const int s0 = T_walk % kStages, s1 = (T_walk + 1) % kStages;
-        if (T_walk < T_end) {
-            if (helper) stage_ring(c0, B, b0, lane, R, ring, cts + s0 * kTile, qls + s0 * 2 * kTile, nars + s0, cy);
-            if (dstw || dsth) stage_dst(c0, lane, dst + s0 * kDstLevels * kTile);
-        }
+        if (T_walk < T_end) stage_ring(c0, B, b0, lane, R, ring, cts + s0 * kTile, qls + s0 * 2 * kTile, nars + s0, cy);
         __syncthreads();
-        if (T_walk + 1 < T_end) {
-            if (helper) stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, nars + s1, cy);
-            if (dstw || dsth) stage_dst(c1, lane, dst + s1 * kDstLevels * kTile);
-        }
+        if (T_walk + 1 < T_end)
+            stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, nars + s1, cy);
     } else {
         __syncthreads();
     }
     if (T_walk < T_end)
         stage_keys(T_walk * kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw,
-                   keys + (T_walk & 1) * nwp * kKS, ctr, (uint32_t)T_walk, nwaves, lane);
+                   keys + (T_walk & 1) * nwp * kKS, ctr, (uint32_t)T_walk, nwaves, lane,
+                   cts + (T_walk % kStages) * kTile, dst + (T_walk % kDstStages) * kDstLevels * kTile);
     __syncthreads();
 
     SmaAcct a;
@@ -509,7 +532,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     a.R = a.gap = a.mdd = 0;
     a.ps1 = a.ps2 = 0;
     a.h = 0;
-    a.s1 = a.s2 = 0;
+    a.s1.clear();
+    a.s2.clear();
     a.agg = kAggId;
     a.A = 0;
     a.Bq = a.C = a.D = kNegInf;
@@ -529,7 +553,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         a.Bq = a.C = a.D = kNegInf;
         a.ntr = 0;
         a.h = 0;
-        a.s1 = a.s2 = 0;
+        a.s1.clear();
+        a.s2.clear();
         a.ps1 = a.ps2 = 0;
         a.e0 = -1;
         a.x1 = -1;
@@ -538,6 +563,14 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     };
     if (SEG && T_walk == T_acct) enter_acct();
     bt_trade* tr = nullptr;
+    // the result index; recomputed after the walk (result_index) so that neither it nor kf / ks
+    // stay live through the tile loop for it
+    auto result_index = [&]() -> size_t {
+        int le = lane;
+        asm volatile("" : "+v"(le));  // opaque: not merged with the value computed above
+        const int je = blockIdx.y * nparam_threads + wave * 64 + le;
+        return (size_t)blockIdx.x * P + (size_t)((je % nf) * ns + je / nf);
+    };
     const size_t gi = (size_t)blockIdx.x * P + p;
     if (PARITY && active) tr = out.trades + gi * out.trade_cap;
     const int cap = out.trade_cap;
@@ -563,14 +596,12 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             const int t0 = k * kTile;
             // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
             // (tile k+1) on every wave, balanced dynamically
-            if ((helper || dstw) && k + 2 < T_end && !BT_ABL(g, 1)) {
-                // stage 1 is a dependent DPP/fp64 chain on one or two waves: issue it first
+            if (helper && k + 2 < T_end && !BT_ABL(g, 1)) {
+                // stage 1 is a dependent DPP/fp64 chain on one wave: issue it first
                 if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
                 const int s = (k + 2) % kStages;
-                if (helper)
-                    stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
-                               qls + s * 2 * kTile, nars + s, cy);
-                if (dstw || dsth) stage_dst(cpre, lane, dst + s * kDstLevels * kTile);
+                stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+                           qls + s * 2 * kTile, nars + s, cy);
                 cpre = load_close(crow, B, t0 + 3 * kTile + lane);
                 __builtin_amdgcn_s_setprio(0);
             }
@@ -585,7 +616,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
                 const int s = k % kStages;
                 const int32_t* cT = cts + s * kTile;
                 const int64_t* ql = qls + s * 2 * kTile;
-                const Agg* D = dst + s * kDstLevels * kTile;
+                const Agg* D = dst + (k % kDstStages) * kDstLevels * kTile;
                 const int32_t* K = keys + (k & 1) * nwp * kKS;
                 const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
                 const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
@@ -631,6 +662,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
                         // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
                         // so the tie is settled in int64 for every grid the engine accepts
                         const double top = ring[(t + 1) & (R - 1)];
+                        const int fw = (int)(fsw & 0xffffu), sw = (int)(fsw >> 16);
                         const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
                         const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
                         G |= (uint64_t)(Fs > Lf) << b;
@@ -683,8 +715,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
                 // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
                 // zero price), so the uint64 partials are exact as int64
                 if ((k & 1) || k + 1 == T_end) {
-                    a.s1 += (i128)(int64_t)a.ps1;
-                    a.s2 += (i128)(int64_t)a.ps2;
+                    a.s1.add((int64_t)a.ps1);
+                    a.s2.add((int64_t)a.ps2);
                     a.ps1 = a.ps2 = 0;
                 }
                 BT_STAMP(5)
@@ -692,7 +724,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             }
             if (k + 1 < T_end && !BT_ABL(g, 2))
                 stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
-                           ctr, (uint32_t)(k + 1), nwaves, lane);
+                           ctr, (uint32_t)(k + 1), nwaves, lane, cts + ((k + 1) % kStages) * kTile,
+                           dst + ((k + 1) % kDstStages) * kDstLevels * kTile);
             BT_STAMP(1)
             __syncthreads();
             BT_STAMP(6)
@@ -745,17 +778,17 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             r.C = a.C;
             r.D = a.D;
             r.h = a.h;
-            r.s1lo = (uint64_t)a.s1;
-            r.s1hi = (int64_t)(a.s1 >> 64);
-            r.s2lo = (uint64_t)a.s2;
-            r.s2hi = (int64_t)(a.s2 >> 64);
+            r.s1lo = a.s1.lo;
+            r.s1hi = a.s1.hi64();
+            r.s2lo = a.s2.lo;
+            r.s2hi = a.s2.hi64();
             *mine = r;
         }
         return;
     }
     if (active) {
-        const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
-        const int64_t s1hi = (int64_t)(a.s1 >> 64), s2hi = (int64_t)(a.s2 >> 64);
+        const uint64_t s1lo = a.s1.lo, s2lo = a.s2.lo;
+        const int64_t s1hi = a.s1.hi64(), s2hi = a.s2.hi64();
         const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, B, g.sqrt_ann);
         bt_summary r;
         r.n_trades = a.ntr;
@@ -766,9 +799,10 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         r.exposure = a.ntr > 0 ? B - 1 - a.e0 : 0;
         r.sharpe = sh;
         r.hash = a.h;
-        out.sum[gi] = r;
-        out.key[gi] = order_key(sh);
-        if (out.sums != nullptr) out.sums[gi] = bt_sums{s1lo, s1hi, s2lo, s2hi};
+        const size_t go = result_index();
+        out.sum[go] = r;
+        out.key[go] = order_key(sh);
+        if (out.sums != nullptr) out.sums[go] = bt_sums{s1lo, s1hi, s2lo, s2hi};
     }
     wave_add_trades(out, active ? a.ntr : 0);
 }
