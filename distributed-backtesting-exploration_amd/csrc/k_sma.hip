@@ -593,142 +593,142 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     // int64 accounts, so each walk keeps its own registers.
     auto tile_step = [&](auto narrow_tag, const int k) __attribute__((always_inline)) {
         constexpr bool NARROW = decltype(narrow_tag)::value;
-            const int t0 = k * kTile;
-            // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
-            // (tile k+1) on every wave, balanced dynamically
-            if (helper && k + 2 < T_end && !BT_ABL(g, 1)) {
-                // stage 1 is a dependent DPP/fp64 chain on one wave: issue it first
-                if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
-                const int s = (k + 2) % kStages;
-                stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
-                           qls + s * 2 * kTile, nars + s, cy);
-                cpre = load_close(crow, B, t0 + 3 * kTile + lane);
-                __builtin_amdgcn_s_setprio(0);
+        const int t0 = k * kTile;
+        // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
+        // (tile k+1) on every wave, balanced dynamically
+        if (helper && k + 2 < T_end && !BT_ABL(g, 1)) {
+            // stage 1 is a dependent DPP/fp64 chain on one wave: issue it first
+            if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
+            const int s = (k + 2) % kStages;
+            stage_ring(cpre, B, t0 + 2 * kTile, lane, R, ring, cts + s * kTile,
+                       qls + s * 2 * kTile, nars + s, cy);
+            cpre = load_close(crow, B, t0 + 3 * kTile + lane);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        BT_STAMP(0)
+        // ---- stage 3 (tile k)
+        if (SEG && active && k == T_acct && k != T_walk) enter_acct();
+        if (active) {
+            // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
+            // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
+            // blocks are ~1 % slower with it)
+            if (ONE_TRIP) __builtin_amdgcn_s_setprio(1);
+            const int s = k % kStages;
+            const int32_t* cT = cts + s * kTile;
+            const int64_t* ql = qls + s * 2 * kTile;
+            const Agg* D = dst + (k % kDstStages) * kDstLevels * kTile;
+            const int32_t* K = keys + (k & 1) * nwp * kKS;
+            const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
+            const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
+            uint32_t l0 = 0, l1 = 0, z = ~0u;
+            if (!BT_ABL(g, 4)) {
+                // all reads at immediate offsets from one address per row
+#pragma unroll
+                for (int v = 0; v < 16; ++v) {
+                    if (v < 8) cmp4(l0, z, k1[v], k2[v]);
+                    else cmp4(l1, z, k1[v], k2[v]);
+                    // keep the schedule to two int4 pairs in flight (VGPR budget)
+                    if (v & 1) __builtin_amdgcn_sched_barrier(0);
+                }
             }
-            BT_STAMP(0)
-            // ---- stage 3 (tile k)
-            if (SEG && active && k == T_acct && k != T_walk) enter_acct();
-            if (active) {
-                // blocks of more than 8 waves (one per CU): compare and walk at raised priority over
-                // the keys / scan work of other waves (config 5 156.4 -> 151.0 ms; config 2's 8-wave
-                // blocks are ~1 % slower with it)
-                if (ONE_TRIP) __builtin_amdgcn_s_setprio(1);
-                const int s = k % kStages;
-                const int32_t* cT = cts + s * kTile;
-                const int64_t* ql = qls + s * 2 * kTile;
-                const Agg* D = dst + (k % kDstStages) * kDstLevels * kTile;
-                const int32_t* K = keys + (k & 1) * nwp * kKS;
-                const int4* k1 = reinterpret_cast<const int4*>(K + kf * kKS);
-                const int4* k2 = reinterpret_cast<const int4*>(K + ks * kKS);
-                uint32_t l0 = 0, l1 = 0, z = ~0u;
-                if (!BT_ABL(g, 4)) {
-                    // all reads at immediate offsets from one address per row
-    #pragma unroll
-                    for (int v = 0; v < 16; ++v) {
-                        if (v < 8) cmp4(l0, z, k1[v], k2[v]);
-                        else cmp4(l1, z, k1[v], k2[v]);
-                        // keep the schedule to two int4 pairs in flight (VGPR budget)
-                        if (v & 1) __builtin_amdgcn_sched_barrier(0);
-                    }
+            BT_STAMP(2)
+            uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
+            const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
+            const int wb = warm - t0;
+            const int bl = B - 1 - t0;       // forced exit: flat after bar B-1
+            uint64_t LONG, F;
+            if (z != 0 && wb <= 0 && lastdec >= 63) {
+                // every bar decides and no keys are equal: the position after bar b is simply
+                // long iff fast > slow (LONG = G = ~L), and the flips are its changes
+                LONG = ~L;
+                F = (LONG ^ ((LONG << 1) | (uint64_t)(a.pos == 1))) | (uint64_t)(a.pos == 0);
+            } else {
+                uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
+                vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
+                uint64_t G, T = 0;
+                if (z != 0) {
+                    G = ~L & vm;
+                } else {  // some bar has equal floor keys: settle those exactly
+                    const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
+                    G = ~(L | E) & vm;
+                    T = E & vm;
                 }
-                BT_STAMP(2)
-                uint64_t L = ((uint64_t)__builtin_bitreverse32(l1) << 32) | __builtin_bitreverse32(l0);
-                const int lastdec = B - 2 - t0;  // decisions only at t <= B-2, from the warm bar on
-                const int wb = warm - t0;
-                const int bl = B - 1 - t0;       // forced exit: flat after bar B-1
-                uint64_t LONG, F;
-                if (z != 0 && wb <= 0 && lastdec >= 63) {
-                    // every bar decides and no keys are equal: the position after bar b is simply
-                    // long iff fast > slow (LONG = G = ~L), and the flips are its changes
-                    LONG = ~L;
-                    F = (LONG ^ ((LONG << 1) | (uint64_t)(a.pos == 1))) | (uint64_t)(a.pos == 0);
-                } else {
-                    uint64_t vm = lastdec >= 63 ? ~0ULL : (lastdec < 0 ? 0ULL : ((1ULL << (lastdec + 1)) - 1));
-                    vm &= wb <= 0 ? ~0ULL : (wb >= 64 ? 0ULL : (~0ULL << wb));
-                    uint64_t G, T = 0;
-                    if (z != 0) {
-                        G = ~L & vm;
-                    } else {  // some bar has equal floor keys: settle those exactly
-                        const uint64_t E = eq_word(K + kf * kKS, K + ks * kKS);
-                        G = ~(L | E) & vm;
-                        T = E & vm;
-                    }
-                    L &= vm;
-                    while (T) {
-                        const int b = __builtin_ctzll(T);
-                        T &= T - 1;
-                        const int t = t0 + b;
-                        // window sums are exact in the ring (< 2^53) and < 2^31 w; F s and L f
-                        // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
-                        // so the tie is settled in int64 for every grid the engine accepts
-                        const double top = ring[(t + 1) & (R - 1)];
-                        const int fw = (int)(fsw & 0xffffu), sw = (int)(fsw >> 16);
-                        const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
-                        const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
-                        G |= (uint64_t)(Fs > Lf) << b;
-                        L |= (uint64_t)(Fs < Lf) << b;
-                    }
-                    // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
-                    uint64_t SHORT;
-                    {
-                        const uint64_t A = ~L;
-                        const uint64_t s1 = A + G;
-                        uint64_t cout = s1 < A;
-                        const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
-                        cout |= sum < s1;
-                        LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
-                    }
-                    {
-                        const uint64_t A = ~G;
-                        const uint64_t s1 = A + L;
-                        uint64_t cout = s1 < A;
-                        const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
-                        cout |= sum < s1;
-                        SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
-                    }
-                    if (bl < 64) {
-                        const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
-                        LONG &= keep;
-                        SHORT &= keep;
-                    }
-                    const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
-                    const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
-                    F = (LONG ^ pL) | (SHORT ^ pS);
+                L &= vm;
+                while (T) {
+                    const int b = __builtin_ctzll(T);
+                    T &= T - 1;
+                    const int t = t0 + b;
+                    // window sums are exact in the ring (< 2^53) and < 2^31 w; F s and L f
+                    // are < 2^31 f s < 2^59 for any windows the LDS ring can hold (< 2^14),
+                    // so the tie is settled in int64 for every grid the engine accepts
+                    const double top = ring[(t + 1) & (R - 1)];
+                    const int fw = (int)(fsw & 0xffffu), sw = (int)(fsw >> 16);
+                    const int64_t Fs = (int64_t)(top - ring[(t + 1 - fw) & (R - 1)]) * sw;
+                    const int64_t Lf = (int64_t)(top - ring[(t + 1 - sw) & (R - 1)]) * fw;
+                    G |= (uint64_t)(Fs > Lf) << b;
+                    L |= (uint64_t)(Fs < Lf) << b;
                 }
-                BT_STAMP(3)
-                uint64_t Fw = F;
-                if (BT_ABL(g, 8)) {  // profiling: drop the trade events (keep F live)
-                    asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
-                    Fw = 0;
+                // set/reset latches via add-with-carry: carry into bit b+1 == position after bar b
+                uint64_t SHORT;
+                {
+                    const uint64_t A = ~L;
+                    const uint64_t s1 = A + G;
+                    uint64_t cout = s1 < A;
+                    const uint64_t sum = s1 + (uint64_t)(a.pos == 1);
+                    cout |= sum < s1;
+                    LONG = ((sum ^ A ^ G) >> 1) | (cout << 63);
                 }
-                sma_flips<PARITY, ONE_TRIP, SEG, NARROW>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
-                BT_STAMP(4)
-                if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
-                    a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
-                    a.sb = 0;
-                    const uint64_t q63 = (uint64_t)ql[kTile - 1];
-                    a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
-                    a.ps2 += (uint64_t)ql[2 * kTile - 1];
+                {
+                    const uint64_t A = ~G;
+                    const uint64_t s1 = A + L;
+                    uint64_t cout = s1 < A;
+                    const uint64_t sum = s1 + (uint64_t)(a.pos == -1);
+                    cout |= sum < s1;
+                    SHORT = ((sum ^ A ^ L) >> 1) | (cout << 63);
                 }
-                // fold the return partials into int128 every second tile (and at the last): over
-                // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
-                // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
-                // zero price), so the uint64 partials are exact as int64
-                if ((k & 1) || k + 1 == T_end) {
-                    a.s1.add((int64_t)a.ps1);
-                    a.s2.add((int64_t)a.ps2);
-                    a.ps1 = a.ps2 = 0;
+                if (bl < 64) {
+                    const uint64_t keep = bl <= 0 ? 0ULL : ((1ULL << bl) - 1);
+                    LONG &= keep;
+                    SHORT &= keep;
                 }
-                BT_STAMP(5)
-                if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
+                const uint64_t pL = (LONG << 1) | (uint64_t)(a.pos == 1);
+                const uint64_t pS = (SHORT << 1) | (uint64_t)(a.pos == -1);
+                F = (LONG ^ pL) | (SHORT ^ pS);
             }
-            if (k + 1 < T_end && !BT_ABL(g, 2))
-                stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
-                           ctr, (uint32_t)(k + 1), nwaves, lane, cts + ((k + 1) % kStages) * kTile,
-                           dst + ((k + 1) % kDstStages) * kDstLevels * kTile);
-            BT_STAMP(1)
-            __syncthreads();
-            BT_STAMP(6)
+            BT_STAMP(3)
+            uint64_t Fw = F;
+            if (BT_ABL(g, 8)) {  // profiling: drop the trade events (keep F live)
+                asm volatile("" ::"v"((uint32_t)Fw), "v"((uint32_t)(Fw >> 32)));
+                Fw = 0;
+            }
+            sma_flips<PARITY, ONE_TRIP, SEG, NARROW>(a, Fw, t0, bl, LONG, cT, ql, D, tr, cap);
+            BT_STAMP(4)
+            if (a.pos != 0) {  // open at the tile end: path so far, returns to the tile end
+                a.agg = agg_merge(a.agg, dst_query_bf(D, a.sb, kTile - 1));
+                a.sb = 0;
+                const uint64_t q63 = (uint64_t)ql[kTile - 1];
+                a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
+                a.ps2 += (uint64_t)ql[2 * kTile - 1];
+            }
+            // fold the return partials into int128 every second tile (and at the last): over
+            // 128 bars |sum pos q| and sum q2 stay below 2^63 (|q|, q2 <= 2^56 by spec §3, and not
+            // all 128 can reach it: that needs |ret| = 1 at every bar, i.e. 128 doublings or a
+            // zero price), so the uint64 partials are exact as int64
+            if ((k & 1) || k + 1 == T_end) {
+                a.s1.add((int64_t)a.ps1);
+                a.s2.add((int64_t)a.ps2);
+                a.ps1 = a.ps2 = 0;
+            }
+            BT_STAMP(5)
+            if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
+        }
+        if (k + 1 < T_end && !BT_ABL(g, 2))
+            stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
+                       ctr, (uint32_t)(k + 1), nwaves, lane, cts + ((k + 1) % kStages) * kTile,
+                       dst + ((k + 1) % kDstStages) * kDstLevels * kTile);
+        BT_STAMP(1)
+        __syncthreads();
+        BT_STAMP(6)
     };
     int k = T_walk;
     if (!SEG && k < T_end) {
