@@ -5,7 +5,7 @@
 //   -> collect: records whose 24-bit prefix is above the selected one (< k of them) and the
 //      candidates that share it -> finish: one block sorts them in LDS by
 //      (key desc, sym asc, param asc) and writes the k result records.
-// Seven small launches, no host round trip; the host reads the count and k records in one copy. The order
+// Six small launches (the finish block also resets the selection state), no host round trip; the host reads the count and k records in one copy. The order
 // is exact and deterministic (atomics only decide collection order, which the sort removes).
 // If more than kCap records tie on the 24-bit prefix (a tie-heavy grid), the finish block
 // completes the exact selection on the device itself (topk_finish_ties), so the result never
@@ -229,7 +229,7 @@ __device__ int topk_finish_ties(const uint64_t* __restrict__ key, int64_t nrec,
 __global__ __launch_bounds__(256) void topk_finish(
     const uint64_t* __restrict__ key, const bt_summary* __restrict__ sum,
     const SymDesc* __restrict__ syms, int64_t nrec, int32_t P,
-    const unsigned long long* __restrict__ state, const unsigned int* __restrict__ counts,
+    unsigned long long* __restrict__ state, unsigned int* __restrict__ counts,
     const unsigned long long* __restrict__ above, const unsigned long long* __restrict__ cand,
     int cap, int32_t k, bt_topk_rec* __restrict__ out, int32_t* __restrict__ out_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -288,16 +288,14 @@ __global__ __launch_bounds__(256) void topk_finish(
         const bt_summary& r = sum[ix[i]];
         out[i] = bt_topk_rec{r.sharpe, (int32_t)(ss[i] >> 32), (int32_t)(uint32_t)ss[i], r.pnl};
     }
-    if (threadIdx.x == 0) out_n[0] = take;
-}
-
-// Reset the selection state for the next run (the histogram is left zeroed by topk_select).
-__global__ void topk_reset(unsigned long long* state, unsigned int* counts) {
+    __syncthreads();  // every read of state / counts is done: reset them for the next chain
     if (threadIdx.x == 0) {
+        out_n[0] = take;
         state[0] = state[1] = state[2] = 0;
         counts[0] = counts[1] = 0;
     }
 }
+
 
 __global__ void topk_init(unsigned long long* state, unsigned int* counts, unsigned int* hist) {
     for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[i] = 0;
@@ -312,7 +310,8 @@ hipError_t launch_topk_init(const TopkWork& w, hipStream_t st) {
     return hipGetLastError();
 }
 
-// The chain assumes the state left by topk_init or by the previous chain's topk_reset.
+// The chain assumes the state left by topk_init or by the previous chain's finish; the
+// histogram is left zeroed by topk_select.
 hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms, int64_t n,
                        int32_t P, int32_t k, const TopkWork& w, hipStream_t st) {
     if (n <= 0 || k <= 0) return hipSuccess;
@@ -333,9 +332,7 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
     // one small block (256 threads, the sort's 2,048 slots in 48 KB of LDS): it finds room on a CU
     // beside the next step's strategy kernel sooner than a 1,024-thread block
     hipLaunchKernelGGL(topk_finish, dim3(1), dim3(256), (size_t)w.cap * 24, st, key, sum, syms,
-                       n, P, (const unsigned long long*)w.state, w.counts, w.above, w.cand, w.cap,
-                       k, w.out, w.out_n);
-    hipLaunchKernelGGL(topk_reset, dim3(1), dim3(64), 0, st, w.state, w.counts);
+                       n, P, w.state, w.counts, w.above, w.cand, w.cap, k, w.out, w.out_n);
     return hipGetLastError();
 }
 
