@@ -66,7 +66,7 @@ constexpr int kLH = 6 * kTile + 16;
 constexpr int kLhBx = 2 * kTile, kLhSuf = 2 * kTile + 16, kLhTs = 4 * kTile + 16;
 
 struct TileLds {
-    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levp, levf, lvb, rec, nrec, ctr, total;
+    size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levp, levf, lvb, rec, nrec, nar, ctr, total;
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
@@ -94,6 +94,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         // trade records [pair][tile & 1][record][lane] and records per lane [pair][tile & 1][lane]
         L.rec = take((size_t)nsplit * 2 * kRecCap * kTile * 2);
         L.nrec = take((size_t)nsplit * 2 * kTile);
+        L.nar = take((size_t)ns * 4);  // per tile stage: the accountant's sums fit int32 (Acct32)
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
@@ -753,6 +754,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // tile later
     uint16_t* recs = reinterpret_cast<uint16_t*>(smem + LL.rec);
     uint8_t* nrec = reinterpret_cast<uint8_t*>(smem + LL.nrec);
+    int32_t* nars = reinterpret_cast<int32_t*>(smem + LL.nar);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     // wave_map: role of hardware wave w < 8 (4 bits each; the roles below are logical wave
@@ -792,6 +794,10 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int itp = jl % g.nd, isl = (jl / g.nd) % g.nc, iw = (jl / (g.nd * g.nc)) % nw,
               ik = jl / (g.nd * g.nc * nw);
     const int pj = ((iw * nk + ik) * g.nc + isl) * g.nd + itp;
+    // an opaque copy for the result write after the walk (not recomputed there from the index's
+    // parts, which would keep two sign-extended pairs live across the walk)
+    int pj_out = pj;
+    asm volatile("" : "+v"(pj_out));
     const int w = g.a[iw];
     const int32_t sl_bps = g.c[isl], tp_bps = g.d[itp];
     const int32_t* crow = close + sd.off;
@@ -865,7 +871,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
         const int s = T % kBollStages, t0 = T * kTile;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
-                                      dst + s * kDstLevels * kTile, cy);
+                                      dst + s * kDstLevels * kTile, cy, true, SEG ? nullptr : nars + s);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (double)pre;  // exact: < 2^31 x 2^22 bars
         // sum of c^2 (< 2^62) as its parts above and below bit 31, each prefix < 2^53
@@ -1127,11 +1133,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // given D / ql of its tile and the trade's sparse-table query index qi (the bar before a
     // fill, the exit bar of a signal exit): the path is the carried aggregate (kAggId for a
     // trade opened in this tile), the tile's closes [a.sb, qi] and the fill price.
-    auto close_trade = [&](int t0, int x, int qi, int32_t px, const Agg& seg, int64_t qx, int64_t q2x) {
+    auto close_trade = [&](auto narrow_tag, Acct32& n32, int t0, int x, int qi, int32_t px,
+                           const Agg& seg, int64_t qx, int64_t q2x) {
+        constexpr bool NARROW = decltype(narrow_tag)::value;
         const bool lg = a.pos > 0;
         const Agg sp = qi < a.sb ? kAggId : seg;
         const Agg st = agg_merge(agg_merge(a.agg, sp), agg_one(px));
-        acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
+        acct_close<PARITY, SEG, NARROW>(a, n32, t0 + x, px, st, tr, cap);
         a.ps1 += lg ? (uint64_t)qx : (uint64_t)0 - (uint64_t)qx;
         a.ps2 += (uint64_t)q2x;
         a.pos = 0;
@@ -1337,37 +1345,51 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int32_t* PH = PL + nlev * kTile;
             const uint16_t* RB = recs + (ka & 1) * kRecCap * kTile + lane;
             const int n = nrec[(ka & 1) * kTile + lane];
+            // the records' accounts in int32 while the closes' total variation allows (Acct32);
+            // one copy of the loop per width, chosen per tile (wave-uniform)
+            auto records = [&](auto narrow_tag) {
+                constexpr bool NARROW = decltype(narrow_tag)::value;
+                Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd};  // gap, mdd <= TV < 2^30 if NARROW
 #pragma unroll 1
-            for (int i = 0; i < n; ++i) {
-                if (STAMPS) sa.count(3);
-                const uint32_t rec = RB[i * kTile];
-                const int b = (int)(rec & 63u), x = (int)((rec >> 8) & 63u), kind = (int)(rec >> 14);
-                if (rec & 64u) {  // entry at b
-                    const int np = (rec & 128u) ? 1 : -1;
-                    const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
-                    const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
-                    const int32_t cx = cT[b];
-                    const int64_t qx = ql[b], q2x = ql[kTile + b];
-                    const int32_t pl = PL[rl], ph = PH[rh];
-                    asm volatile("" ::"v"(cx), "v"(qx), "v"(q2x), "v"(pl), "v"(ph));
-                    a.ps1 += np > 0 ? (uint64_t)0 - (uint64_t)qx : (uint64_t)qx;
-                    a.ps2 -= (uint64_t)q2x;
-                    acct_open(a, ta + b, b, cx);
-                    a.pos = np;
-                    XL = pl;
-                    XHm1 = ph;
+                for (int i = 0; i < n; ++i) {
+                    if (STAMPS) sa.count(3);
+                    const uint32_t rec = RB[i * kTile];
+                    const int b = (int)(rec & 63u), x = (int)((rec >> 8) & 63u), kind = (int)(rec >> 14);
+                    if (rec & 64u) {  // entry at b
+                        const int np = (rec & 128u) ? 1 : -1;
+                        const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
+                        const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
+                        const int32_t cx = cT[b];
+                        const int64_t qx = ql[b], q2x = ql[kTile + b];
+                        const int32_t pl = PL[rl], ph = PH[rh];
+                        asm volatile("" ::"v"(cx), "v"(qx), "v"(q2x), "v"(pl), "v"(ph));
+                        a.ps1 += np > 0 ? (uint64_t)0 - (uint64_t)qx : (uint64_t)qx;
+                        a.ps2 -= (uint64_t)q2x;
+                        acct_open(a, ta + b, b, cx);
+                        a.pos = np;
+                        XL = pl;
+                        XHm1 = ph;
+                    }
+                    if (kind != 0) {  // exit at x
+                        const bool hit = kind >= 2;
+                        const int qi = hit ? x - 1 : x;
+                        const Agg seg = dst_query_w(D, a.sb, max(qi, a.sb));
+                        const int32_t cxx = cT[x];
+                        const int64_t qx = ql[x], q2x = ql[kTile + x];
+                        asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
+                        const int32_t px = hit ? (kind == 2 ? XL : XHm1 + 1) : cxx;
+                        close_trade(narrow_tag, n32, ta, x, qi, px, seg, qx, q2x);
+                    }
                 }
-                if (kind != 0) {  // exit at x
-                    const bool hit = kind >= 2;
-                    const int qi = hit ? x - 1 : x;
-                    const Agg seg = dst_query_w(D, a.sb, max(qi, a.sb));
-                    const int32_t cxx = cT[x];
-                    const int64_t qx = ql[x], q2x = ql[kTile + x];
-                    asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
-                    const int32_t px = hit ? (kind == 2 ? XL : XHm1 + 1) : cxx;
-                    close_trade(ta, x, qi, px, seg, qx, q2x);
+                if (NARROW) {
+                    a.gap = (uint32_t)n32.g;  // >= 0
+                    a.mdd = (uint32_t)n32.m;
                 }
-            }
+            };
+            if (!SEG && __builtin_amdgcn_readfirstlane(nars[s]))
+                records(std::true_type{});
+            else
+                records(std::false_type{});
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
@@ -1391,7 +1413,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         if (keeps) seg_write(a, start_pos, start_e, sg.rec + (size_t)sr.seg * gridDim.x * P + (size_t)blockIdx.x * P + pje);
         return;
     }
-    if (keeps) acct_write(a, B, g.sqrt_ann, gi, out);
+    if (keeps) acct_write(a, B, g.sqrt_ann, (size_t)blockIdx.x * P + pj_out, out);
     wave_add_trades(out, keeps ? a.ntr : 0);
 }
 

@@ -23,6 +23,8 @@ constexpr int kTileStages = 3;  // tile buffers in flight: scanned (k+2), flagge
 struct TileCarry {
     int64_t P;       // sum of closes before the tile
     int32_t prevc;   // close of the bar before the tile
+    uint32_t tv;     // total variation of the closes up to the tile, saturated at 2^31 (narrow
+                     // accounts, Acct32)
 };
 
 // One whole wave, lane = bar t0 + lane, c = its close (0 past the end): writes the tile's
@@ -31,7 +33,7 @@ struct TileCarry {
 // inclusive prefix sum of closes up to this lane's bar (exact int64).
 __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane, int32_t* cT,
                                              int64_t* ql, Agg* D, TileCarry& cy,
-                                             bool with_dst = true) {
+                                             bool with_dst = true, int32_t* narrow = nullptr) {
     const int t = t0 + lane;
     const bool valid = t < B;
     const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
@@ -40,9 +42,19 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     const int64_t pre = cy.P + inc;
     cT[lane] = c;
     int64_t q = 0, q2 = 0;
-    if (valid && t >= 1) fixed_ret(c, cp, q, q2);
+    uint32_t dv = 0;  // |c_t - c_(t-1)|
+    if (valid && t >= 1) {
+        fixed_ret(c, cp, q, q2);
+        dv = (uint32_t)abs(c - cp);
+    }
     ql[lane] = wave_iscan_i64(q);
     ql[kTile + lane] = wave_iscan_i64(q2);
+    if (narrow != nullptr) {  // the tile's total variation and the narrow flag (Acct32)
+        const bool big = __ballot(dv >= (1u << 25)) != 0;
+        const uint32_t tvt = __builtin_amdgcn_readlane(wave_iscan_u32(min(dv, 1u << 25)), 63);
+        cy.tv = big ? (1u << 31) : min(cy.tv + tvt, 1u << 31);
+        if (lane == 0) *narrow = cy.tv < (1u << 30);
+    }
     cy.P += lane63_i64(inc);
     cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
     if (with_dst) dst_build(c, lane, D);  // (profiling ablation only: false skips the table)
@@ -85,11 +97,21 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
 // Close the open trade (a.pos, a.e, a.ce) at global bar t for price px, given the trade's
 // adverse / favourable excursions lo / hi and internal drawdown `path` (all relative to the
 // entry close, in the trade's direction), its pnl and its hash term mix(w).
-template <bool PARITY, bool SEG = false>
-__device__ __forceinline__ void acct_fold(TradeAcct& a, int t, int32_t px, int32_t lo, int32_t hi,
-                                          int32_t path, int32_t pnl, uint64_t mix, bt_trade* tr,
-                                          int cap) {
-    if (SEG) {
+// Narrow accounts: while the closes' total variation TV (through the tile's last bar) is below
+// 2^30, gap and mdd — differences of equity or price values, |.| <= TV, and the recursion's
+// intermediates <= 2 TV — are exact in int32 (k_sma.hip SmaAcct has the argument).
+struct Acct32 {
+    int32_t g, m;  // gap, mdd
+};
+
+template <bool PARITY, bool SEG = false, bool NARROW = false>
+__device__ __forceinline__ void acct_fold(TradeAcct& a, Acct32& n, int t, int32_t px, int32_t lo,
+                                          int32_t hi, int32_t path, int32_t pnl, uint64_t mix,
+                                          bt_trade* tr, int cap) {
+    if (NARROW && !SEG) {
+        n.m = max(n.m, max(n.g - lo, path));
+        n.g = max(n.g, hi) - pnl;
+    } else if (SEG) {
         const int64_t A0 = a.A, B0 = a.Bq;
         a.C = max(a.C, A0 - (int64_t)lo);
         a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
@@ -122,15 +144,22 @@ __device__ __forceinline__ uint64_t trade_term(int e, int t, bool lg) {
 
 // Close the open trade at global bar t for price px; `st` aggregates the trade's whole price
 // path in order, exit point included.
-template <bool PARITY, bool SEG = false>
-__device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
+template <bool PARITY, bool SEG = false, bool NARROW = false>
+__device__ __forceinline__ void acct_close(TradeAcct& a, Acct32& n, int t, int32_t px, const Agg& st,
                                            bt_trade* tr, int cap) {
     const bool lg = a.pos > 0;
     const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;  // |.| < 2^31
     const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
     const int32_t path = lg ? st.dd : st.du;
     const int32_t pnl = lg ? px - a.ce : a.ce - px;
-    acct_fold<PARITY, SEG>(a, t, px, lo, hi, path, pnl, trade_term(a.e, t, lg), tr, cap);
+    acct_fold<PARITY, SEG, NARROW>(a, n, t, px, lo, hi, path, pnl, trade_term(a.e, t, lg), tr, cap);
+}
+
+template <bool PARITY, bool SEG = false>
+__device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
+                                           bt_trade* tr, int cap) {
+    Acct32 unused{0, 0};
+    acct_close<PARITY, SEG, false>(a, unused, t, px, st, tr, cap);
 }
 
 __device__ __forceinline__ void acct_open(TradeAcct& a, int t, int b, int32_t px) {

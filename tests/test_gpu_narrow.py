@@ -82,3 +82,33 @@ def test_sma_narrow_to_wide_accounts_match_oracle(parity):
             compare_summary(got[s, p], orc[p], where)
             if parity:
                 compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parity", [False, True])
+def test_boll_narrow_to_wide_accounts_match_oracle(parity):
+    """The Bollinger kernel's accountant (the split walk of the busiest z threshold) keeps gap and
+    mdd in int32 on the same total-variation bound (tile_common.h Acct32); the same series, with
+    highs and lows around the closes, through the config-4 grid."""
+    grid = D.config4_grid()
+    rng = np.random.default_rng(7)
+    closes = _series()
+    highs = [np.clip(c.astype(np.int64) + rng.integers(0, 1 << 16, len(c)), 1, 2**31 - 1).astype(np.int32)
+             for c in closes]
+    lows = [np.clip(c.astype(np.int64) - rng.integers(0, 1 << 16, len(c)), 1, 2**31 - 1).astype(np.int32)
+            for c in closes]
+    kw = dict(parity=True, trade_cap=CAP) if parity else {}
+    with D.Engine(grid, **kw) as e:
+        e.set_segments(1)                     # whole-series walks: the narrow path is SEG-free
+        e.load_ohlc(closes, highs, lows)
+        e.run()
+        assert e.last_segments() == 1
+        got = e.summaries()
+        tr = e.trades() if parity else None
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("boll", grid, (cl, highs[s], lows[s], cl), 98280, CAP if parity else 0)
+        for p in range(grid.n_params):
+            where = f"boll series {s} (first wide tile {_first_wide_tile(cl)}) {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            if parity:
+                compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
