@@ -382,16 +382,36 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         // three dependent fp64 operations per bar; raising its priority over the walk no longer
         // pays (the walk, tasks, scan and chain all set the tile together: DESIGN.md §4.2)
         if (!BT_ABL(g, 32)) set_prio(BT_PRIO(g, 16, kEmaChainPrio));
+        // the tile's closes as doubles, staged in span 0's row (lane = bar): each bar's close is
+        // then one broadcast LDS read issued ahead of the chain instead of a readlane and a
+        // conversion on it; span 0 overwrites bar b only after every span has read it (one
+        // wave, LDS in program order)
+        const double* CD = ebuf + (T & 1) * estage;
+        if (nsp > 0) ebuf[(T & 1) * estage + lane] = (double)cl;
         if (lane < nsp && !BT_ABL(g, 256)) {  // profiling: 256 drops the chain, 128 its math
             if (BT_ABL(g, 128)) {
 #pragma unroll
                 for (int b = 0; b < kTile; ++b) E[b] = (double)__builtin_amdgcn_readlane(cl, b);
             } else if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
+                // 8 bars' closes read one chunk ahead (the reads precede, in program order, the
+                // chain's stores that may alias them)
+                double nx[8];
 #pragma unroll
-                for (int b = 0; b < kTile; ++b) {
-                    const double cd = (double)__builtin_amdgcn_readlane(cl, b);
-                    ema = ema + alpha * (cd - ema);
-                    E[b] = ema;
+                for (int u = 0; u < 8; ++u) nx[u] = CD[u];
+#pragma unroll
+                for (int c = 0; c < kTile / 8; ++c) {
+                    double cur[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) cur[u] = nx[u];
+                    if (c + 1 < kTile / 8) {
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) nx[u] = CD[8 * (c + 1) + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        ema = ema + alpha * (cur[u] - ema);
+                        E[8 * c + u] = ema;
+                    }
                 }
             } else {
 #pragma unroll 1
