@@ -174,6 +174,9 @@ def main():
                     help="bar segments per symbol (bt_set_segments): 0 = automatic, 1 = off")
     ap.add_argument("--burn", type=int, default=0,
                     help="burn-in tiles of a speculative segment: 0 = the strategy's default")
+    ap.add_argument("--verify", action="store_true",
+                    help="after timing, rank 0 runs every rank's symbols in one engine and asserts "
+                         "that the exchanged top-k and counters equal it (N > 1 rehearsals)")
     args = ap.parse_args()
     if args.leg == "ingest":
         return ingest_leg(args)
@@ -235,30 +238,29 @@ def main():
             eng.topk_fetch_async(i & 1)       # its top-k + trade count into pinned slot i % 2
 
     def finish(i):
+        """(top-k, [bar-evals, trades]) of step i over every rank."""
         if topk == 0:
-            return None
+            return None, None
         if comm is not None:
-            top, _ = comm.exchange_wait(i & 1)
-            return top
+            return comm.exchange_wait(i & 1)
         top, trades = eng.topk_fetch_wait(i & 1)
         if dist is None:
-            return top
+            return top, [n_sym * BARS * P, trades]
         # the one exchange step: a single all-gather carrying each rank's k x 24 B top-k records
-        # and its run counters (summed on the host)
-        top, _ = PAR.exchange(top, TOPK, [n_sym * BARS * P, trades], dist)
-        return top
+        # and its run counters (summed on the host), in the C-ABI exchange's byte format
+        return PAR.exchange(top, topk, [n_sym * BARS * P, trades], dist)
 
     def steps(n):
         """n steps; step i+1 is enqueued before step i's read-back and exchange, so the GPU runs
         the next pass while the host consumes (and, for N > 1, exchanges) this one."""
-        top = None
+        res = (None, None)
         if n > 0:
             issue(0)
         for i in range(n):
             if i + 1 < n:
                 issue(i + 1)
-            top = finish(i)
-        return top
+            res = finish(i)
+        return res
 
     steps(args.warmup)
     eng.sync()
@@ -268,7 +270,7 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    top = steps(args.steps)
+    top, counters = steps(args.steps)
     eng.sync()
     if dist is not None:
         torch.cuda.synchronize()
@@ -284,6 +286,10 @@ def main():
     # bar segments per symbol of the last run and the blocks its fix passes re-walked (read
     # after the timed region: the count is a device read-back)
     n_seg, refixed = eng.last_segments(with_refixed=True)
+
+    verified = None
+    if args.verify and rank == 0 and topk > 0:
+        verified = verify_exchange(cfg, grid, total, top, counters, device, topk, args)
 
     if rank == 0:
         evals_per_step = total * BARS * P
@@ -331,10 +337,13 @@ def main():
                          "pmc_source": pmc.get("source") if same_shard else None,
                          "kernel": kname, "kernel_avg_ms": kavg_s * 1e3},
             "trades_per_step": stats["trades"],
+            "trades_per_step_all_ranks": counters[1] if counters else None,
             "bar_segments": {"per_symbol": n_seg, "refixed_blocks_last_step": refixed},
             "top1": {"sharpe": float(top[0]["sharpe"]), "sym": int(top[0]["sym"]),
                      "param": int(top[0]["param"])} if top is not None and len(top) else None,
         }
+        if verified is not None:
+            line["verified_exchange"] = verified
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg, grid, sym0, n_sym)
         print(json.dumps(line), flush=True)
@@ -343,6 +352,25 @@ def main():
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def verify_exchange(cfg, grid, total, top, counters, device, k, args):
+    """Rank 0, after the timed region: one engine over every rank's symbols (0 .. total-1) on this
+    GPU; the exchanged top-k must equal its device top-k record for record, and the summed
+    counters its bar-evals and trade count. Raises on a mismatch (a nonzero exit)."""
+    ref = D.Engine(grid, device=device, topk=k)
+    if args.segments or args.burn:
+        ref.set_segments(args.segments, args.burn)
+    ref.load_synthetic(SEED, 0, total, cfg["B"], cfg["freq"])
+    ref.run()
+    want = ref.read_topk(k)
+    st = ref.stats()
+    ref.close()
+    got = np.asarray(top, D.TOPK_DTYPE)
+    assert got.tobytes() == np.asarray(want, D.TOPK_DTYPE).tobytes(), \
+        f"exchanged top-{k} differs from a single engine over all {total} symbols"
+    assert counters == [st["bar_evals"], st["trades"]], (counters, st)
+    return {"symbols": total, "topk": len(got), "bar_evals": counters[0], "trades": counters[1]}
 
 
 def ingest_leg(args):

@@ -9,12 +9,21 @@
 // latency-bound, so it is a single ncclAllGather on the engine's top-k stream, enqueued behind
 // the run's top-k chain without a host wait, and read back into one of two pinned slots so the
 // next run overlaps it (the same pipelining as bt_topk_fetch_async / bt_topk_fetch_wait).
+//
+// RCCL is resolved with dlopen on the first communicator call, not linked: a single-GPU worker
+// (configs 1-2) loads libbt.so on a box without librccl (the reference's worker build hook,
+// /root/reference/build.rs:1-4, links nothing either). rccl.h is used for its types only. In a
+// process that already holds an RCCL (PyTorch-ROCm's bundled librccl.so, SONAME librccl.so.1),
+// dlopen by SONAME returns that copy, as the dynamic linker did when libbt.so linked it.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "internal.h"
@@ -45,15 +54,91 @@ struct CommFail {
         if (e_ != hipSuccess) throw CommFail{std::string(#x) + ": " + hipGetErrorString(e_)}; \
     } while (0)
 
+// the RCCL entry points this file calls
+struct Rccl {
+    void* so = nullptr;
+    std::string why;  // dlopen / dlsym failure
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (const char* name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"}) {
+            r.so = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (r.so) break;
+        }
+        if (!r.so) {
+            const char* e = dlerror();
+            r.why = std::string("RCCL is not loadable (librccl.so.1): ") + (e ? e : "dlopen failed");
+            return;
+        }
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(r.so, name));
+            if (!fn && r.why.empty()) r.why = std::string("RCCL lacks ") + name;
+        };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.AllGather, "ncclAllGather");
+        sym(r.GetErrorString, "ncclGetErrorString");
+    });
+    if (!r.why.empty()) throw CommFail{r.why};
+    return r;
+}
+
 #define NCCLCHK(x)                                                                             \
     do {                                                                                       \
         ncclResult_t r_ = (x);                                                                 \
-        if (r_ != ncclSuccess) throw CommFail{std::string(#x) + ": " + ncclGetErrorString(r_)}; \
+        if (r_ != ncclSuccess)                                                                 \
+            throw CommFail{std::string(#x) + ": " + rccl().GetErrorString(r_)};               \
     } while (0)
 
 // Per-rank message: header record (record count in its first int32), k records, then the two
 // int64 counters (bar-evals, trades).
 size_t message_bytes(int32_t k) { return ((size_t)k + 1) * sizeof(bt_topk_rec) + 2 * sizeof(int64_t); }
+
+// The host half of bt_exchange_wait: merge `world` gathered messages of k_msg records each.
+int32_t merge_block(const unsigned char* block, int32_t world, int32_t k_msg, bt_topk_rec* out,
+                    int32_t k, int64_t* counters) {
+    const size_t mb = message_bytes(k_msg);
+    std::vector<bt_topk_rec> all;
+    all.reserve((size_t)k_msg * world);
+    int64_t evals = 0, trades = 0;
+    for (int32_t r = 0; r < world; ++r) {
+        const unsigned char* m = block + (size_t)r * mb;
+        int32_t n = 0;
+        memcpy(&n, m, sizeof n);
+        // every rank's device selection is exact whatever the ties (k_topk.hip
+        // topk_finish_ties), so a tie-heavy grid exchanges like any other
+        if (n < 0) throw CommFail{"rank " + std::to_string(r) + ": bad top-k record count"};
+        n = std::min(n, k_msg);
+        const unsigned char* recs = m + sizeof(bt_topk_rec);
+        for (int32_t i = 0; i < n; ++i) {  // memcpy: the block carries no alignment promise
+            bt_topk_rec x;
+            memcpy(&x, recs + (size_t)i * sizeof x, sizeof x);
+            all.push_back(x);
+        }
+        int64_t x[2];
+        memcpy(x, m + ((size_t)k_msg + 1) * sizeof(bt_topk_rec), sizeof x);
+        evals += x[0];
+        trades += x[1];
+    }
+    const size_t mm = std::min<size_t>(all.size(), (size_t)std::min(k, k_msg));
+    std::partial_sort(all.begin(), all.begin() + mm, all.end(), topk_less);
+    std::copy(all.begin(), all.begin() + mm, out);
+    if (counters) {
+        counters[0] = evals;
+        counters[1] = trades;
+    }
+    return (int32_t)mm;
+}
 
 void release(bt_comm* c) {
     if (!c) return;
@@ -61,7 +146,7 @@ void release(bt_comm* c) {
     for (int s = 0; s < 2; ++s) {
         if (c->done[s]) (void)hipEventSynchronize(c->done[s]);
     }
-    if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->comm) (void)rccl().CommDestroy(c->comm);  // comm set: rccl() resolved
     if (c->d_send) (void)hipFree(c->d_send);
     for (int s = 0; s < 2; ++s) {
         if (c->d_recv[s]) (void)hipFree(c->d_recv[s]);
@@ -80,7 +165,7 @@ int32_t bt_comm_unique_id(uint8_t* out) {
     try {
         if (!out) throw CommFail{"null output"};
         ncclUniqueId id;
-        NCCLCHK(ncclGetUniqueId(&id));
+        NCCLCHK(rccl().GetUniqueId(&id));
         static_assert(sizeof(id) == BT_COMM_ID_BYTES, "RCCL unique id size");
         memcpy(out, &id, sizeof id);
         return 0;
@@ -105,10 +190,11 @@ bt_comm* bt_comm_create(const uint8_t* id, int32_t rank, int32_t world, int32_t 
         c->device = device;
         c->k = k;
         c->rec_bytes = message_bytes(k);
+        const Rccl& nc = rccl();
         HIPCHK(hipSetDevice(device));
         ncclUniqueId uid;
         memcpy(&uid, id, sizeof uid);
-        NCCLCHK(ncclCommInitRank(&c->comm, world, uid, rank));
+        NCCLCHK(nc.CommInitRank(&c->comm, world, uid, rank));
         HIPCHK(hipMalloc(&c->d_send, c->rec_bytes));
         for (int s = 0; s < 2; ++s) {
             HIPCHK(hipMalloc(&c->d_recv[s], c->rec_bytes * world));
@@ -152,7 +238,8 @@ int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot) {
         HIPCHK(hipMemcpyAsync(cnt + sizeof(int64_t), v.d_ntr, sizeof(int64_t), hipMemcpyDeviceToDevice,
                               v.tstream));
         engine_exchange_enqueued(e);
-        NCCLCHK(ncclAllGather(c->d_send, c->d_recv[slot], c->rec_bytes, ncclChar, c->comm, v.tstream));
+        NCCLCHK(rccl().AllGather(c->d_send, c->d_recv[slot], c->rec_bytes, ncclChar, c->comm,
+                                 v.tstream));
         HIPCHK(hipMemcpyAsync(c->h_recv[slot], c->d_recv[slot], c->rec_bytes * c->world,
                               hipMemcpyDeviceToHost, v.tstream));
         HIPCHK(hipEventRecord(c->done[slot], v.tstream));
@@ -175,32 +262,23 @@ int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipEventSynchronize(c->done[slot]));
         c->armed[slot] = false;
-        std::vector<bt_topk_rec> all;
-        all.reserve((size_t)c->k * c->world);
-        int64_t evals = 0, trades = 0;
-        for (int32_t r = 0; r < c->world; ++r) {
-            const unsigned char* m = c->h_recv[slot] + (size_t)r * c->rec_bytes;
-            int32_t n = 0;
-            memcpy(&n, m, sizeof n);
-            // every rank's device selection is exact whatever the ties (k_topk.hip
-            // topk_finish_ties), so a tie-heavy grid exchanges like any other
-            if (n < 0) throw CommFail{"rank " + std::to_string(r) + ": bad top-k record count"};
-            n = std::min(n, c->k);
-            const bt_topk_rec* recs = reinterpret_cast<const bt_topk_rec*>(m) + 1;
-            all.insert(all.end(), recs, recs + n);
-            int64_t x[2];
-            memcpy(x, m + ((size_t)c->k + 1) * sizeof(bt_topk_rec), sizeof x);
-            evals += x[0];
-            trades += x[1];
-        }
-        const size_t mm = std::min<size_t>(all.size(), (size_t)std::min(k, c->k));
-        std::partial_sort(all.begin(), all.begin() + mm, all.end(), topk_less);
-        std::copy(all.begin(), all.begin() + mm, out);
-        if (counters) {
-            counters[0] = evals;
-            counters[1] = trades;
-        }
-        return (int32_t)mm;
+        return merge_block(c->h_recv[slot], c->world, c->k, out, k, counters);
+    } catch (const CommFail& f) {
+        set_last_error(f.msg);
+        return -1;
+    } catch (...) {
+        set_last_error("unknown exception");
+        return -1;
+    }
+}
+
+int64_t bt_exchange_message_bytes(int32_t k) { return k < 1 ? -1 : (int64_t)message_bytes(k); }
+
+int32_t bt_exchange_merge(const uint8_t* block, int32_t world, int32_t k_msg, bt_topk_rec* out,
+                          int32_t k, int64_t* counters) {
+    try {
+        if (!block || world < 1 || k_msg < 1 || !out || k < 1) throw CommFail{"bad arguments"};
+        return merge_block(block, world, k_msg, out, k, counters);
     } catch (const CommFail& f) {
         set_last_error(f.msg);
         return -1;

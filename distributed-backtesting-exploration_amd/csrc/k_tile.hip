@@ -890,8 +890,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
 
     auto scan = [&](int T, int32_t c, int32_t hv, int32_t lv) {
         const int s = T % kBollStages, t0 = T * kTile;
-        const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
-                                      dst + s * kDstLevels * kTile, cy, true, SEG ? nullptr : nars + s);
+        const int64_t pre = tile_scan<true>(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
+                                            dst + s * kDstLevels * kTile, cy, true,
+                                            SEG ? nullptr : nars + s, hv, lv);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (double)pre;  // exact: < 2^31 x 2^22 bars
         // sum of c^2 (< 2^62) as its parts above and below bit 31, each prefix < 2^53

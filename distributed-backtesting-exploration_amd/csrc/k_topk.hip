@@ -240,6 +240,9 @@ __global__ __launch_bounds__(256) void topk_finish(
     const int n_above = (int)counts[0], n_cand = (int)counts[1];
     int n = n_above + n_cand;
     const bool ties = n > cap;
+    // the tie histogram borrows the cap key slots (cap = kTopkCap, engine.cpp)
+    static_assert(kTopkCap * sizeof(uint64_t) >= kBins * sizeof(unsigned int),
+                  "topk_finish_ties' histogram must fit the key slots");
     if (ties) {  // the histogram (16 KB) borrows the key slots, filled only after the gather
         // state[2]: records still wanted from the prefix group (k minus those above it)
         n = topk_finish_ties(key, nrec, syms, P, state[0], state[1], state[2], k,

@@ -27,13 +27,34 @@ struct TileCarry {
                      // accounts, Acct32)
 };
 
+// Level fills (Bollinger SL/TP, HL = true): a trade closed by its stop-loss or take-profit fills
+// at the level price px, not at a close, so the equity path the narrow bound needs is the close
+// path with px inserted before c_t at every such exit. That adds at most 2 dist(px, [min(c_(t-1),
+// c_t), max(c_(t-1), c_t)]) to the total variation, and the distance is bounded by the bar data
+// alone: a long stop at bar t fills at XL >= l_t (the low touched it) with XL <= c_(t-1) (else
+// l_(t-1) <= c_(t-1) < XL had stopped it a bar earlier, or t-1 is the entry bar, c = ce >= XL), so
+// dist <= min(c_(t-1), c_t) - l_t; a long take-profit likewise <= h_t - max(c_(t-1), c_t); shorts
+// mirror. Bars with l > c or h < c (the parser does not order OHLC) break the "a bar earlier"
+// step by at most l_(t-1) - c_(t-1) or c_(t-1) - h_(t-1). So each bar adds twice
+//   max(0, min(c_(t-1), c_t) - l_t) + max(0, h_t - max(c_(t-1), c_t)) + max(0, l_t - c_t)
+//   + max(0, c_t - h_t)
+// to TV (each term clamped at 2^24; synthetic bars: about twice the h/l offsets, ~1 % of TV).
+__device__ __forceinline__ uint32_t level_fill_slack(int32_t c, int32_t cp, int32_t hv, int32_t lv) {
+    const int64_t mlo = min(c, cp), mhi = max(c, cp), C = c, H = hv, L = lv;
+    auto cl = [](int64_t x) { return (uint32_t)min(max(x, (int64_t)0), (int64_t)1 << 24); };
+    return cl(mlo - L) + cl(H - mhi) + cl(L - C) + cl(C - H);
+}
+
 // One whole wave, lane = bar t0 + lane, c = its close (0 past the end): writes the tile's
 // closes cT[64], the in-tile prefixes of the fixed-point returns ql[0..63] (q) and
 // ql[64..127] (q2), and the disjoint sparse table D[6][64] of the close path. Returns the
-// inclusive prefix sum of closes up to this lane's bar (exact int64).
+// inclusive prefix sum of closes up to this lane's bar (exact int64). With HL, the bar's high
+// and low (hv, lv) add their level-fill slack to the narrow bound's total variation.
+template <bool HL = false>
 __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane, int32_t* cT,
                                              int64_t* ql, Agg* D, TileCarry& cy,
-                                             bool with_dst = true, int32_t* narrow = nullptr) {
+                                             bool with_dst = true, int32_t* narrow = nullptr,
+                                             int32_t hv = 0, int32_t lv = 0) {
     const int t = t0 + lane;
     const bool valid = t < B;
     const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
@@ -42,11 +63,13 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     const int64_t pre = cy.P + inc;
     cT[lane] = c;
     int64_t q = 0, q2 = 0;
-    uint32_t dv = 0;  // |c_t - c_(t-1)|
+    uint32_t dv = 0;  // |c_t - c_(t-1)| (+ the level-fill slack, HL)
     if (valid && t >= 1) {
         fixed_ret(c, cp, q, q2);
         dv = (uint32_t)abs(c - cp);
     }
+    if (HL && narrow != nullptr && valid)  // dv < 2^31, twice the slack <= 2^27: no wrap
+        dv += 2 * level_fill_slack(c, t >= 1 ? cp : c, hv, lv);
     ql[lane] = wave_iscan_i64(q);
     ql[kTile + lane] = wave_iscan_i64(q2);
     if (narrow != nullptr) {  // the tile's total variation and the narrow flag (Acct32)

@@ -80,7 +80,8 @@ def split_off_n_jobs(files: List[str], n: int) -> Optional[List[str]]:
 
 class Dispatcher:
     def __init__(self, paths: List[str], prune_after_s: float = 10.0, check_every_s: float = 0.1,
-                 results_path: Optional[str] = None, max_reply_bytes: int = 60 << 20):
+                 results_path: Optional[str] = None, max_reply_bytes: int = 60 << 20,
+                 oversize_drop_after: int = 3):
         self.files = list(paths)
         self.n_paths = len(set(paths))
         self.files_lock = threading.Lock()
@@ -93,6 +94,10 @@ class Dispatcher:
         self.done_paths: Dict[str, str] = {}   # path -> id of its first completion
         self.requeued = 0
         self.oversize_skips = 0  # replies that could not carry their first file (receive limit)
+        # a file above every connected worker's receive limit is dropped (failed, logged) after
+        # this many such skips, so all_done() / --exit-when-done still finish
+        self.oversize_drop_after = oversize_drop_after
+        self._oversize_by_path: Dict[str, int] = {}
         self.failed_paths: List[str] = []     # unreadable / undeliverable (counted done)
         self.done_lock = threading.Lock()
         self.results_path = results_path
@@ -187,9 +192,14 @@ class Dispatcher:
                 self.done_paths[path] = None
                 self.failed_paths.append(path)
 
-    def request_jobs(self, req, ctx):
+    def _no_peer_can_take(self, need: int) -> bool:
         with self.peers_lock:
-            self.peers[ctx.peer()] = {"status": P.IDLE, "last_connection": time.time()}
+            return all(need > p.get("cap", 0) for p in self.peers.values())
+
+    def request_jobs(self, req, ctx):
+        cap = self._reply_cap(ctx)
+        with self.peers_lock:
+            self.peers[ctx.peer()] = {"status": P.IDLE, "last_connection": time.time(), "cap": cap}
         with self.files_lock:
             files = split_off_n_jobs(self.files, req.cores)
         if files is None:
@@ -199,7 +209,6 @@ class Dispatcher:
             ctx.abort(grpc.StatusCode.NOT_FOUND, "No more jobs available")
         jobs = []
         size = 0
-        cap = self._reply_cap(ctx)
         for i, path in enumerate(files):
             jid = str(uuid.uuid4())
             try:
@@ -216,11 +225,19 @@ class Dispatcher:
             if size + need > cap:
                 # too large for what is left of this reply, or for this worker's receive limit
                 # altogether: back to the queue, for a later request or a worker with a larger
-                # limit (--max-receive-mb) to take
+                # limit (--max-receive-mb) to take; dropped once it has been skipped
+                # oversize_drop_after times while no connected worker's limit admits it
+                rest = files[i:]
+                if not jobs and need > cap:
+                    self.oversize_skips += 1
+                    n = self._oversize_by_path[path] = self._oversize_by_path.get(path, 0) + 1
+                    if n >= self.oversize_drop_after and self._no_peer_can_take(need):
+                        log.error("%s (%d bytes) exceeds every connected worker's receive limit "
+                                  "after %d requests: dropped", path, len(data), n)
+                        self._drop_unreadable(path)
+                        rest = files[i + 1:]
                 with self.files_lock:
-                    self.files.extend(files[i:])
-                    if not jobs and need > cap:
-                        self.oversize_skips += 1
+                    self.files.extend(rest)
                 break
             size += need
             with self.done_lock:

@@ -157,6 +157,9 @@ def lib():
     L.bt_comm_destroy.restype = None
     L.bt_exchange_async.argtypes = [P, P, C.c_int32]
     L.bt_exchange_wait.argtypes = [P, C.c_int32, P, C.c_int32, P]
+    L.bt_exchange_message_bytes.argtypes = [C.c_int32]
+    L.bt_exchange_message_bytes.restype = C.c_int64
+    L.bt_exchange_merge.argtypes = [P, C.c_int32, C.c_int32, P, C.c_int32, P]
     L.bt_last_batch_profile.argtypes = [P, C.POINTER(_BatchProfile)]
     L.bt_format_summaries.argtypes = [P, C.c_int32, P, C.c_size_t]
     L.bt_format_summaries.restype = C.c_int64
@@ -461,6 +464,31 @@ def merge_topk(records: np.ndarray, k: int) -> np.ndarray:
     m = _check(lib().bt_merge_topk(recs.ctypes.data if len(recs) else None, len(recs), k,
                                    out.ctypes.data))
     return out[:m]
+
+
+def exchange_message(records: np.ndarray, k_msg: int, bar_evals: int, trades: int) -> bytes:
+    """One rank's exchange message as bt_exchange_async sends it (comm.cpp): a header record whose
+    first int32 is the record count, k_msg record slots (the first n used), bar-evals, trades."""
+    n = len(records)
+    size = _check(lib().bt_exchange_message_bytes(k_msg))
+    buf = np.zeros(size, np.uint8)
+    buf[:4] = np.frombuffer(np.int32(n).tobytes(), np.uint8)
+    rec = TOPK_DTYPE.itemsize
+    if n:
+        buf[rec:rec * (1 + n)] = np.frombuffer(np.ascontiguousarray(records, TOPK_DTYPE).tobytes(), np.uint8)
+    buf[rec * (k_msg + 1):] = np.frombuffer(np.array([bar_evals, trades], np.int64).tobytes(), np.uint8)
+    return buf.tobytes()
+
+
+def exchange_merge(block: bytes, world: int, k_msg: int, k: int) -> tuple:
+    """The host half of Comm.exchange_wait (bt_exchange_merge) on a gathered block of `world`
+    messages: the merged top-k and [bar-evals, trades] summed over ranks."""
+    raw = np.frombuffer(block, np.uint8)
+    out = np.zeros(max(k, 1), TOPK_DTYPE)
+    cnt = np.zeros(2, np.int64)
+    m = _check(lib().bt_exchange_merge(raw.ctypes.data, world, k_msg, out.ctypes.data, k,
+                                       cnt.ctypes.data))
+    return out[:m], [int(cnt[0]), int(cnt[1])]
 
 
 def format_summaries(rows: np.ndarray) -> str:

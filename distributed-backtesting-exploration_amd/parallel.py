@@ -47,25 +47,23 @@ def gather_topk(local: np.ndarray, k: int, dist) -> np.ndarray:
 
 
 def exchange(local: np.ndarray, k: int, counters, dist) -> tuple:
-    """The whole per-step exchange as ONE all-gather: each rank contributes
-    [k records (3 int64 words each) | record count | counters...], so the top-k merge and the
-    counter sum need a single latency-bound collective over xGMI instead of three.
+    """The whole per-step exchange as ONE all-gather of the byte message bt_exchange_async sends
+    over RCCL (csrc/comm.cpp: [header record with the count | k records | bar-evals | trades]),
+    merged by the same C function bt_exchange_wait calls (bt_exchange_merge). This is the
+    torch.distributed carrier of that exchange: the fallback when the C-ABI communicator cannot
+    be created, and the rehearsal with ranks sharing one GPU (gloo), so the world > 1 parse and
+    merge run the product code either way. counters = [bar-evals, trades].
     Returns (merged top-k, summed counters)."""
     import torch
+    from .engine import exchange_merge, exchange_message
     world = dist.get_world_size()
-    nc = len(counters)
-    buf = np.zeros(3 * k + 1 + nc, np.int64)
+    evals, trades = (int(v) for v in counters)
     n = min(len(local), k)
-    buf[:3 * n] = np.asarray(local, TOPK_DTYPE)[:n].view(np.int64)
-    buf[3 * k] = n
-    buf[3 * k + 1:] = [int(v) for v in counters]
-    t = torch.from_numpy(buf).to(_device_for(dist))
-    out = torch.empty(world * buf.size, dtype=torch.int64, device=t.device)
+    msg = exchange_message(np.asarray(local, TOPK_DTYPE)[:n], k, evals, trades)
+    t = torch.frombuffer(bytearray(msg), dtype=torch.uint8).to(_device_for(dist))
+    out = torch.empty(world * len(msg), dtype=torch.uint8, device=t.device)
     dist.all_gather_into_tensor(out, t)
-    g = out.cpu().numpy().reshape(world, buf.size)
-    parts = [g[r, :3 * int(g[r, 3 * k])].view(TOPK_DTYPE) for r in range(world)]
-    top = merge_topk(np.concatenate(parts) if parts else np.zeros(0, TOPK_DTYPE), k)
-    return top, [int(x) for x in g[:, 3 * k + 1:].sum(axis=0)]
+    return exchange_merge(out.cpu().numpy().tobytes(), world, k, k)
 
 
 def make_comm(dist, device: int, k: int):

@@ -237,7 +237,29 @@ class Worker:
             th.join(timeout=5)
             for f in fetch:
                 f.join(timeout=5)
+            self._flush_retries()
             self.channel.close()
+
+    def _flush_retries(self):
+        """On stop: one last attempt for every completion still waiting for a retry (and any
+        queued one); what still fails is logged with its job id, since the dispatcher re-runs
+        those jobs only after it prunes this worker."""
+        pending = list(self._retry)
+        self._retry = []
+        while True:
+            try:
+                pending.append(self.complete_q.get_nowait() + (0.0, 0))
+            except queue.Empty:
+                break
+        lost = []
+        for jid, data, _, _ in pending:
+            try:
+                self._complete(P.CompleteRequest(id=jid, data=data))
+            except grpc.RpcError:
+                lost.append(jid)
+        if lost:
+            log.warning("Stopping with %d completions undelivered (the dispatcher re-runs them "
+                        "once it prunes this worker): %s", len(lost), ", ".join(lost))
 
     def _send_completions(self):
         """Send every ready completion. One that fails (the reference unwraps and panics here,

@@ -218,7 +218,10 @@ int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* o
  * bt_exchange_async enqueues the exchange of the engine's last run (which needs topk >= k) into
  * pinned slot 0 or 1 behind the run's top-k chain, without a host wait; bt_exchange_wait returns
  * the merged global top-k (count) and counters[2] = {bar-evals, trades} summed over ranks.
- * Every rank must issue the same sequence of exchanges. */
+ * Every rank must issue the same sequence of exchanges.
+ * RCCL is loaded at run time (dlopen of librccl.so.1 on the first bt_comm_unique_id /
+ * bt_comm_create): libbt.so does not link it, so a single-GPU host loads the engine without RCCL,
+ * and these two calls fail with "RCCL is not loadable" there. */
 #define BT_COMM_ID_BYTES 128
 typedef struct bt_comm bt_comm;
 int32_t bt_comm_unique_id(uint8_t* out);
@@ -228,6 +231,14 @@ void bt_comm_destroy(bt_comm* c);
 int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot);
 int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
                          int64_t* counters);
+/* The host half of bt_exchange_wait, callable without a GPU: `block` holds `world` messages of
+ * bt_exchange_message_bytes(k_msg) bytes in rank order, each [header record whose first int32 is
+ * the record count n (clipped to k_msg; < 0 is an error) | k_msg records, the first n sorted |
+ * int64 bar-evals | int64 trades], as the all-gather delivers them. Writes the min(k, k_msg,
+ * sum n) best records in engine order and counters[2] = the summed counters; returns the count. */
+int64_t bt_exchange_message_bytes(int32_t k_msg);
+int32_t bt_exchange_merge(const uint8_t* block, int32_t world, int32_t k_msg, bt_topk_rec* out,
+                          int32_t k, int64_t* counters);
 
 /* ---- self-test hooks (host-side helpers the tests call without a GPU) */
 /* The CompleteRequest.data text of P summaries (spec §6, one JSON line per param), as

@@ -84,6 +84,100 @@ def test_sma_narrow_to_wide_accounts_match_oracle(parity):
                 compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
+def _level_fill_slack(h, lo, c):
+    """tile_common.h level_fill_slack per bar: what an SL/TP fill at a level can add to the
+    close path's total variation (twice this is added to TV)."""
+    c = c.astype(np.int64)
+    h = h.astype(np.int64)
+    lo = lo.astype(np.int64)
+    cp = np.concatenate([c[:1], c[:-1]])
+    mlo, mhi = np.minimum(c, cp), np.maximum(c, cp)
+    cl = lambda x: np.clip(x, 0, 1 << 24)
+    return cl(mlo - lo) + cl(h - mhi) + cl(lo - c) + cl(c - h)
+
+
+def _first_wide_tile_hl(h, lo, c):
+    """The Bollinger scan's rule: per bar |c_t - c_(t-1)| + 2 x the level-fill slack."""
+    d = np.zeros(len(c), np.int64)
+    d[1:] = np.abs(np.diff(c.astype(np.int64)))
+    d += 2 * _level_fill_slack(h, lo, c)
+    tv = 0
+    for k in range((len(c) + 63) // 64):
+        x = d[64 * k:64 * k + 64]
+        tv += (1 << 40) if (x >= (1 << 25)).any() else int(np.minimum(x, 1 << 25).sum())
+        if tv >= (1 << 30):
+            return k
+    return None
+
+
+WICK_BARS = 20_000
+
+
+def _wick_series():
+    """prices near 2^31, closes moving a few hundred ticks a bar (TV ~ 4e6,
+    narrow by the closes alone), and wicks deep enough that every trade stops out at its level:
+    each stop loses ~1e7-2e7 ticks, thousands of them push gap and mdd past 2^31. Series: both
+    sides stopped on every bar; only longs stopped (shorts take normal wicks); deep wicks only
+    from bar 12,000 on (narrow, then wide part-way); invalid bars (low above the close) that
+    stop shorts a bar late."""
+    rng = np.random.default_rng(99)
+    B = WICK_BARS
+    out = []
+    base = (2_000_000_000 + np.cumsum(rng.integers(-400, 401, B))).astype(np.int64)
+    deep_h = np.full(B, 2**31 - 1, np.int64)
+    deep_l = np.full(B, 10_000, np.int64)
+    near_h = base + rng.integers(0, 200, B)
+    near_l = base - rng.integers(0, 200, B)
+    out.append((deep_h, deep_l, base))
+    out.append((near_h, deep_l, base))
+    h3, l3 = near_h.copy(), near_l.copy()
+    h3[12_000:], l3[12_000:] = deep_h[12_000:], deep_l[12_000:]
+    out.append((h3, l3, base))
+    l4 = deep_l.copy()
+    l4[::7] = base[::7] + 3_000_000                      # l > c: the parser does not order OHLC
+    out.append((deep_h, l4, base))
+    return [tuple(x.astype(np.int32) for x in s) for s in out]
+
+
+def test_wick_series_overflow_int32_without_the_level_slack():
+    import orc_ffi as F
+    grid = D.config4_grid()
+    for i, (h, lo, c) in enumerate(_wick_series()):
+        assert _first_wide_tile(c) is None, i           # the closes alone: narrow throughout
+        k = _first_wide_tile_hl(h, lo, c)
+        assert k is not None, i
+        if i == 2:
+            assert 12_000 // 64 <= k < WICK_BARS // 64 - 1, k
+        # the busiest threshold (smallest k, the accountant's wave) runs past 2^31
+        kw = grid.param(0)
+        s, _ = F.boll(h, lo, c, kw["w"], kw["k_num"], kw["k_den"], kw["sl"], kw["tp"], 98280)
+        assert int(s["mdd"]) > (2**29 if i == 1 else 2**31), (i, s)  # 1: short take-profits offset
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parity", [False, True])
+def test_boll_level_fills_keep_wide_accounts(parity):
+    """Stops filled at their levels move equity by ~ce·bps/1e4 however flat the closes are: the
+    narrow flag must count the bars' wicks (tile_common.h level_fill_slack), else the int32
+    accountant overflows. Every field vs the C oracle."""
+    grid = D.config4_grid()
+    series = _wick_series()
+    kw = dict(parity=True, trade_cap=CAP) if parity else {}
+    with D.Engine(grid, **kw) as e:
+        e.set_segments(1)
+        e.load_ohlc([s[2] for s in series], [s[0] for s in series], [s[1] for s in series])
+        e.run()
+        got = e.summaries()
+        tr = e.trades() if parity else None
+    for i, (h, lo, c) in enumerate(series):
+        orc, otr = oracle_row("boll", grid, (c, h, lo, c), 98280, CAP if parity else 0)
+        for p in range(grid.n_params):
+            where = f"wick series {i} {grid.param(p)}"
+            compare_summary(got[i, p], orc[p], where)
+            if parity:
+                compare_trades(tr[i, p], otr[p], min(int(orc[p]["n_trades"]), CAP), where)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("parity", [False, True])
 def test_boll_narrow_to_wide_accounts_match_oracle(parity):

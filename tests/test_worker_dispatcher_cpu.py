@@ -181,6 +181,31 @@ def test_failed_complete_job_is_retried_until_the_dispatcher_is_done(tmp_path):
         d.close()
 
 
+def test_pending_retries_get_a_last_attempt_and_a_log_on_stop(caplog):
+    """ADVICE r3: completions waiting for a retry when the worker stops get one last attempt;
+    what still fails is logged with its job ids instead of vanishing."""
+    import grpc
+    import logging
+    sent = []
+
+    def down(req):
+        if req.id == "j1":
+            sent.append(req.id)
+            return None
+        raise grpc.RpcError("server down")
+    w = WK.Worker("127.0.0.1:1", lambda jobs: ["ok"] * len(jobs), cores=1)
+    w._complete = down
+    try:
+        w._retry = [("j1", "ok", time.monotonic() + 60, 3), ("j2", "ok", time.monotonic() + 60, 3)]
+        w.complete_q.put(("j3", "ok"))
+        with caplog.at_level(logging.WARNING):
+            w._flush_retries()
+        assert sent == ["j1"] and not w._retry
+        assert "2 completions undelivered" in caplog.text and "j2" in caplog.text and "j3" in caplog.text
+    finally:
+        w.channel.close()
+
+
 def test_status_keeps_a_peer_alive():
     """SendStatus from a known peer refreshes its last connection (a throttled fetcher's
     keep-alive), so the health thread does not prune it and re-dispatch its jobs."""
@@ -193,3 +218,38 @@ def test_status_keeps_a_peer_alive():
         assert "stranger" not in d.peers                 # main.rs:80-102: no upsert on status
     finally:
         d.close()
+
+
+def test_file_above_every_workers_limit_is_dropped_after_repeated_skips(tmp_path):
+    """a file within the server's send limit but above every connected worker's
+    receive limit is dropped (failed, logged) after oversize_drop_after skips instead of being
+    requeued forever, so all_done() (--exit-when-done) still becomes true."""
+    big = tmp_path / "big"
+    big.write_bytes(b"y" * 5000)
+    d = DSP.Dispatcher([str(big)], max_reply_bytes=10000, oversize_drop_after=3)
+    try:
+        md = ((P.MAX_RECEIVE_KEY, str(DSP.REPLY_MARGIN + 1000)),)
+        for n in (1, 2):
+            r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))
+            assert len(r.jobs) == 0 and d.files == [str(big)] and not d.all_done(), n
+        r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))
+        assert len(r.jobs) == 0 and not d.files and d.failed_paths == [str(big)]
+        assert d.all_done()
+    finally:
+        d.close()
+
+
+def test_oversize_file_waits_while_a_larger_worker_is_connected(tmp_path):
+    big = tmp_path / "big"
+    big.write_bytes(b"y" * 5000)
+    d = DSP.Dispatcher([str(big)], max_reply_bytes=10000, oversize_drop_after=2)
+    try:
+        md = ((P.MAX_RECEIVE_KEY, str(DSP.REPLY_MARGIN + 1000)),)
+        d.request_jobs(P.JobsRequest(cores=5), _Ctx("b"))            # "b" (4 MiB) takes it...
+        d.files.append(str(big))                                     # ...say it was lost
+        for _ in range(4):
+            r = d.request_jobs(P.JobsRequest(cores=0), _Ctx("a", md))
+            assert len(r.jobs) == 0 and d.files == [str(big)]         # "b" could still take it
+    finally:
+        d.close()
+
