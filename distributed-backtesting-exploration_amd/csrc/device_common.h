@@ -16,6 +16,9 @@ constexpr int kDstLevels = 6;      // log2(kTile)
 constexpr int kKeyStride = kTile + 1;  // +1 double per key row: conflict-free ds_read_b64
 
 typedef __int128 i128;
+// explicit LDS (address space 3) element types, for pointers kept opaque in a VGPR so that
+// accesses use small immediate offsets from it
+typedef __attribute__((address_space(3))) double lds_f64;
 
 // Price-path aggregate over a run of closes, in order: max, min, max drawdown (max over
 // i<=j of c_i - c_j), max draw-up (max over i<=j of c_j - c_i). Prices < 2^31, so every

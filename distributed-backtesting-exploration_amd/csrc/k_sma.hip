@@ -239,20 +239,6 @@ __device__ __forceinline__ uint64_t eq_word(const int32_t* k1, const int32_t* k2
 //    and gap - lo, max(gap, hi) - pnl at most 2 TV. While TV (through the tile's last bar) is
 //    below 2^30, the walk keeps gap / mdd / realized pnl in int32 (g32, m32, r32), exactly; at
 //    the first wider tile they move into the int64 fields for good.
-// A 96-bit signed accumulator (two VGPRs fewer than int128): the Sharpe sums are bounded by
-// 2^22 bars x 2^56 < 2^78 (spec §3), and 2^95 leaves room to spare.
-struct I96 {
-    uint64_t lo;
-    int32_t hi;
-    __device__ __forceinline__ void clear() { lo = 0; hi = 0; }
-    __device__ __forceinline__ void add(int64_t x) {
-        const uint64_t n = lo + (uint64_t)x;
-        hi += (int32_t)(n < lo) - (int32_t)(x < 0);  // carry out of the low word, sign of x
-        lo = n;
-    }
-    __device__ __forceinline__ int64_t hi64() const { return (int64_t)hi; }
-};
-
 struct SmaAcct {
     int32_t pos, e, ce, sb, ntr, e0;     // sb: in-tile bar where the open trade's path resumes;
                                          // e0: first entry bar
@@ -265,7 +251,7 @@ struct SmaAcct {
     // (tile_common.h TradeAcct), and the trade open at the segment start, whose entry lies in an
     // earlier segment: `carried` while it is open, then its exit bar x1, fill px1 and path agg1
     // from the segment start (closed by the combine pass, internal.h SmaSegRec)
-    int64_t A, Bq, C, D;
+    int64_t Bq, C, D;                    // A = -R: both start at 0, R moves by +pnl, A by -pnl
     int32_t carried, x1, px1;
     Agg agg1;
 };
@@ -296,10 +282,9 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int
     const int32_t path = lg ? st.dd : st.du;
     const int32_t pnl = lg ? cx - a.ce : a.ce - cx;
     if (SEG) {
-        const int64_t A0 = a.A, B0 = a.Bq;
+        const int64_t A0 = -a.R, B0 = a.Bq;  // A = -R (SmaAcct)
         a.C = max(a.C, A0 - (int64_t)lo);
         a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
-        a.A = A0 - pnl;
         a.Bq = max(B0, (int64_t)hi) - pnl;
     } else if (NARROW) {  // |.| <= 2 TV < 2^31 (SmaAcct)
         a.m32 = max(a.m32, max(a.g32 - lo, path));
@@ -535,7 +520,6 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     a.s1.clear();
     a.s2.clear();
     a.agg = kAggId;
-    a.A = 0;
     a.Bq = a.C = a.D = kNegInf;
     a.carried = a.x1 = a.px1 = 0;
     a.agg1 = kAggId;
@@ -549,7 +533,6 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         a.agg = kAggId;
         a.sb = 0;
         a.R = 0;
-        a.A = 0;
         a.Bq = a.C = a.D = kNegInf;
         a.ntr = 0;
         a.h = 0;
@@ -773,7 +756,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             r.end_agg[2] = a.agg.dd;
             r.end_agg[3] = a.agg.du;
             r.R = a.R;
-            r.A = a.A;
+            r.A = -a.R;
             r.B = a.Bq;
             r.C = a.C;
             r.D = a.D;

@@ -394,10 +394,16 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 for (int b = 0; b < kTile; ++b) E[b] = (double)__builtin_amdgcn_readlane(cl, b);
             } else if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
                 // 8 bars' closes read one chunk ahead (the reads precede, in program order, the
-                // chain's stores that may alias them)
+                // chain's stores that may alias them). Both rows are addressed from opaque LDS
+                // pointers: with the buffer's constant offset folded into the addresses, every
+                // ds_write2/ds_read2 (8-bit offsets) needed its own v_add / v_mov
+                lds_f64* Ev = (lds_f64*)E;
+                const lds_f64* Cv = (const lds_f64*)CD;
+                asm volatile("" : "+v"(Ev));
+                asm volatile("" : "+v"(Cv));
                 double nx[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) nx[u] = CD[u];
+                for (int u = 0; u < 8; ++u) nx[u] = Cv[u];
 #pragma unroll
                 for (int c = 0; c < kTile / 8; ++c) {
                     double cur[8];
@@ -405,12 +411,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     for (int u = 0; u < 8; ++u) cur[u] = nx[u];
                     if (c + 1 < kTile / 8) {
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) nx[u] = CD[8 * (c + 1) + u];
+                        for (int u = 0; u < 8; ++u) nx[u] = Cv[8 * (c + 1) + u];
                     }
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         ema = ema + alpha * (cur[u] - ema);
-                        E[8 * c + u] = ema;
+                        Ev[8 * c + u] = ema;
                     }
                 }
             } else {
@@ -732,6 +738,12 @@ __device__ __forceinline__ double level_y(double ce, double g) { return ce * g +
 // boundary fix_seg: the block re-walks that segment from the previous segment's end states if
 // any lane's speculative start differs, and otherwise returns at once). Results go to SegRec
 // records (internal.h) that seg_combine folds.
+// bar segments' accountant in int32 while the segment's total variation allows (Acct32 SEG forms)
+#ifndef BT_BOLL_SEG_NARROW
+#define BT_BOLL_SEG_NARROW 0
+#endif
+constexpr bool kBollSegNarrow = BT_BOLL_SEG_NARROW;
+
 template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
                                                          const int32_t* __restrict__ high,
@@ -892,7 +904,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const int s = T % kBollStages, t0 = T * kTile;
         const int64_t pre = tile_scan<true>(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                             dst + s * kDstLevels * kTile, cy, true,
-                                            SEG ? nullptr : nars + s, hv, lv);
+                                            (SEG && fix_seg > 0) ? nullptr : nars + s, hv, lv);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (double)pre;  // exact: < 2^31 x 2^22 bars
         // sum of c^2 (< 2^62) as its parts above and below bit 31, each prefix < 2^53
@@ -1370,7 +1382,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             // one copy of the loop per width, chosen per tile (wave-uniform)
             auto records = [&](auto narrow_tag) {
                 constexpr bool NARROW = decltype(narrow_tag)::value;
-                Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd};  // gap, mdd <= TV < 2^30 if NARROW
+                // gap, mdd (SEG: the forms) within 2 TV < 2^31 if NARROW
+                Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd, 0, 0, 0};
+                if (SEG && NARROW) {
+                    n32.B = form_to32(a.Bq);
+                    n32.C = form_to32(a.C);
+                    n32.D = form_to32(a.D);
+                }
 #pragma unroll 1
                 for (int i = 0; i < n; ++i) {
                     if (STAMPS) sa.count(3);
@@ -1402,12 +1420,17 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         close_trade(narrow_tag, n32, ta, x, qi, px, seg, qx, q2x);
                     }
                 }
-                if (NARROW) {
+                if (NARROW && SEG) {
+                    a.Bq = form_to64(n32.B);
+                    a.C = form_to64(n32.C);
+                    a.D = form_to64(n32.D);
+                } else if (NARROW) {
                     a.gap = (uint32_t)n32.g;  // >= 0
                     a.mdd = (uint32_t)n32.m;
                 }
             };
-            if (!SEG && __builtin_amdgcn_readfirstlane(nars[s]))
+            // the fix pass writes no flags (its injected trade may predate the segment's scan)
+            if ((!SEG || (kBollSegNarrow && fix_seg == 0)) && __builtin_amdgcn_readfirstlane(nars[s]))
                 records(std::true_type{});
             else
                 records(std::false_type{});

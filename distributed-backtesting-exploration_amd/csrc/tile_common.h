@@ -95,25 +95,41 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
 //  * bar segments (SEG): the entering gap g and mdd m are unknown, so the drawdown is kept as
 //    gap = max(g + A, Bq), mdd = max(m, g + C, D): a trade (lo, hi, path, pnl) maps
 //    C' = max(C, A - lo), D' = max(D, Bq - lo, path), A' = A - pnl, Bq' = max(Bq, hi) - pnl.
+//    A starts at 0 with R and moves by -pnl as R moves by +pnl, so A = -R is not stored.
 constexpr int64_t kNegInf = -(1LL << 60);  // "minus infinity" of the max-plus forms
+
+// A 96-bit signed accumulator (two VGPRs fewer than int128): the Sharpe sums are bounded by
+// 2^22 bars x 2^56 < 2^78 (spec §3), and 2^95 leaves room to spare.
+struct I96 {
+    uint64_t lo;
+    int32_t hi;
+    __device__ __forceinline__ void clear() { lo = 0; hi = 0; }
+    __device__ __forceinline__ void add(int64_t x) {
+        const uint64_t n = lo + (uint64_t)x;
+        hi += (int32_t)(n < lo) - (int32_t)(x < 0);  // carry out of the low word, sign of x
+        lo = n;
+    }
+    __device__ __forceinline__ int64_t hi64() const { return (int64_t)hi; }
+};
+
 
 struct TradeAcct {
     int32_t pos, e, ce, sb, ntr, expo;  // sb: in-tile bar where the open trade's path resumes
     int64_t R, gap, mdd;
-    int64_t A, Bq, C, D;                // SEG walks only
+    int64_t Bq, C, D;                   // SEG walks only (A = -R)
     uint64_t ps1, ps2, h;
-    i128 s1, s2;
+    I96 s1, s2;
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
 };
 
 __device__ __forceinline__ void acct_init(TradeAcct& a) {
     a.pos = a.e = a.ce = a.sb = a.ntr = a.expo = 0;
     a.R = a.gap = a.mdd = 0;
-    a.A = 0;
     a.Bq = a.C = a.D = kNegInf;
     a.ps1 = a.ps2 = 0;
     a.h = 0;
-    a.s1 = a.s2 = 0;
+    a.s1.clear();
+    a.s2.clear();
     a.agg = kAggId;
 }
 
@@ -123,22 +139,37 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
 // Narrow accounts: while the closes' total variation TV (through the tile's last bar) is below
 // 2^30, gap and mdd — differences of equity or price values, |.| <= TV, and the recursion's
 // intermediates <= 2 TV — are exact in int32 (k_sma.hip SmaAcct has the argument).
+// Bar segments (SEG) keep the max-plus forms A, B, C, D narrow on the same bound, over the
+// segment's own bars (its scan restarts the total variation; the fix pass, whose injected open
+// trade may predate the scan, stays wide): A = -R in [-TV, TV]; B, D either "minus infinity" or in
+// [0, 2 TV] (a trade's path holds its entry, so lo <= 0 <= hi and hi >= pnl); C either minus
+// infinity or in [-TV, 2 TV]. Minus infinity is kNeg32 = INT32_MIN, and kNeg32 - lo = INT32_MIN
+// + |lo| stays below every real value without wrapping.
 struct Acct32 {
-    int32_t g, m;  // gap, mdd
+    int32_t g, m;        // gap, mdd
+    int32_t B, C, D;     // SEG: the drawdown forms (A = -R)
 };
+constexpr int32_t kNeg32 = INT32_MIN;
+
+__device__ __forceinline__ int32_t form_to32(int64_t x) { return x == kNegInf ? kNeg32 : (int32_t)x; }
+__device__ __forceinline__ int64_t form_to64(int32_t x) { return x == kNeg32 ? kNegInf : (int64_t)x; }
 
 template <bool PARITY, bool SEG = false, bool NARROW = false>
 __device__ __forceinline__ void acct_fold(TradeAcct& a, Acct32& n, int t, int32_t px, int32_t lo,
                                           int32_t hi, int32_t path, int32_t pnl, uint64_t mix,
                                           bt_trade* tr, int cap) {
-    if (NARROW && !SEG) {
+    if (NARROW && SEG) {
+        const int32_t A0 = -(int32_t)a.R, B0 = n.B;  // A = -R (see TradeAcct)
+        n.C = max(n.C, A0 - lo);
+        n.D = max(n.D, max(B0 - lo, path));
+        n.B = max(B0, hi) - pnl;
+    } else if (NARROW) {
         n.m = max(n.m, max(n.g - lo, path));
         n.g = max(n.g, hi) - pnl;
     } else if (SEG) {
-        const int64_t A0 = a.A, B0 = a.Bq;
+        const int64_t A0 = -a.R, B0 = a.Bq;  // A = -R (see TradeAcct)
         a.C = max(a.C, A0 - (int64_t)lo);
         a.D = max(a.D, max(B0 - (int64_t)lo, (int64_t)path));
-        a.A = A0 - pnl;
         a.Bq = max(B0, (int64_t)hi) - pnl;
     } else {
         a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
@@ -181,7 +212,7 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, Acct32& n, int t, int32
 template <bool PARITY, bool SEG = false>
 __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
                                            bt_trade* tr, int cap) {
-    Acct32 unused{0, 0};
+    Acct32 unused{0, 0, 0, 0, 0};
     acct_close<PARITY, SEG, false>(a, unused, t, px, st, tr, cap);
 }
 
@@ -201,15 +232,15 @@ __device__ __forceinline__ void acct_tile_end(TradeAcct& a, const Agg* D, const 
         a.ps1 += a.pos > 0 ? q63 : (uint64_t)0 - q63;
         a.ps2 += (uint64_t)ql[2 * kTile - 1];
     }
-    a.s1 += (i128)(int64_t)a.ps1;
-    a.s2 += (i128)(int64_t)a.ps2;
+    a.s1.add((int64_t)a.ps1);
+    a.s2.add((int64_t)a.ps2);
     a.ps1 = a.ps2 = 0;
 }
 
 __device__ __forceinline__ void acct_write(const TradeAcct& a, int bars, double sqrt_ann,
                                            size_t gi, const Out& out) {
-    const uint64_t s1lo = (uint64_t)a.s1, s2lo = (uint64_t)a.s2;
-    const int64_t s1hi = (int64_t)(a.s1 >> 64), s2hi = (int64_t)(a.s2 >> 64);
+    const uint64_t s1lo = a.s1.lo, s2lo = a.s2.lo;
+    const int64_t s1hi = a.s1.hi64(), s2hi = a.s2.hi64();
     const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, bars, sqrt_ann);
     bt_summary r;
     r.n_trades = a.ntr;
@@ -272,11 +303,11 @@ __device__ __forceinline__ void seg_inject(TradeAcct& a, const SegRec* prev) {
 // First accounted tile: the sums restart (the burn-in's are dropped); the state carries on.
 __device__ __forceinline__ void seg_reset_sums(TradeAcct& a) {
     a.R = 0;
-    a.A = 0;
     a.Bq = a.C = a.D = kNegInf;
     a.ntr = a.expo = 0;
     a.h = 0;
-    a.s1 = a.s2 = 0;
+    a.s1.clear();
+    a.s2.clear();
     a.ps1 = a.ps2 = 0;
 }
 
@@ -295,15 +326,15 @@ __device__ __forceinline__ void seg_write(const TradeAcct& a, int start_pos, int
     r.end_agg[2] = a.agg.dd;
     r.end_agg[3] = a.agg.du;
     r.R = a.R;
-    r.A = a.A;
+    r.A = -a.R;
     r.B = a.Bq;
     r.C = a.C;
     r.D = a.D;
     r.h = a.h;
-    r.s1lo = (uint64_t)a.s1;
-    r.s1hi = (int64_t)(a.s1 >> 64);
-    r.s2lo = (uint64_t)a.s2;
-    r.s2hi = (int64_t)(a.s2 >> 64);
+    r.s1lo = a.s1.lo;
+    r.s1hi = a.s1.hi64();
+    r.s2lo = a.s2.lo;
+    r.s2hi = a.s2.hi64();
     *mine = r;
 }
 
