@@ -377,7 +377,7 @@ void run_impl(bt_engine* e) {
     switch (e->cfg.strategy) {
         case BT_SMA_CROSS: {
             // bar segments (k_sma.hip) for shards of few, long one-block-per-CU symbols
-            SegArgs sg{nullptr, nullptr, nullptr, 1, e->seg_burn_set ? e->seg_burn : kSmaBurnTiles};
+            SegArgs sg{nullptr, nullptr, nullptr, nullptr, 1, e->seg_burn_set ? e->seg_burn : kSmaBurnTiles};
             if (!parity) {
                 int32_t maxb = 0;
                 for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);
@@ -385,7 +385,10 @@ void run_impl(bt_engine* e) {
                                       : sma_auto_segments(S, e->P, maxb, e->grid.wmax, sg.burn_tiles);
             }
             if (sg.G > 1) {
-                e->d_seg.ensure(2 * (size_t)sg.G * S * e->P);  // SmaSegRec: two SegRec slots
+                // one SegRec slot per SmaSegRec, then the int8 start / end position planes
+                const size_t nrec = (size_t)sg.G * S * e->P;
+                e->d_seg.ensure(nrec + (2 * nrec + sizeof(SegRec) - 1) / sizeof(SegRec));
+                sg.pos = reinterpret_cast<int8_t*>(e->d_seg.p + nrec);
                 e->d_refixed.ensure(1);
                 HIPCHK(hipMemsetAsync(e->d_refixed.p, 0, sizeof(unsigned long long), e->stream));
                 sg.rec = e->d_seg.p;
@@ -402,7 +405,7 @@ void run_impl(bt_engine* e) {
             // the default burn-in lets every span's chain meet the true one; an explicit one
             // (bt_set_segments) is honoured, the fix pass covering a short one
             const int32_t burn = e->seg_burn_set ? e->seg_burn : ema_burn_tiles(maxspan);
-            SegArgs sg{nullptr, nullptr, nullptr, 1, burn};
+            SegArgs sg{nullptr, nullptr, nullptr, nullptr, 1, burn};
             if (!parity) sg.G = e->seg_req > 0 ? e->seg_req : ema_auto_segments(S, e->P, maxb, burn);
             if (sg.G > 1) {
                 e->d_seg.ensure((size_t)sg.G * S * e->P);
@@ -418,7 +421,7 @@ void run_impl(bt_engine* e) {
             break;
         }
         case BT_BOLL: {
-            SegArgs sg{nullptr, nullptr, nullptr, 1, e->seg_burn};
+            SegArgs sg{nullptr, nullptr, nullptr, nullptr, 1, e->seg_burn};
             if (!parity) {
                 int32_t maxb = 0;
                 for (const SymDesc& sd : e->syms) maxb = std::max(maxb, sd.bars);

@@ -446,14 +446,16 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     // T_acct, up to T_end (exclusive); all tiles without SEG
     SegRange sr{0, 0, 0, 0, ntiles};
     SmaSegRec* mine = nullptr;
-    const SmaSegRec* prev = nullptr;
+    size_t ipos = 0, npos = 0;  // this lane's slot in the position planes, their size
     if (SEG) {
         sr = seg_range(sg, fix_seg, ntiles, g.wmax);
         const size_t per_seg = (size_t)gridDim.x * P;
-        mine = reinterpret_cast<SmaSegRec*>(sg.rec) + sr.seg * per_seg + (size_t)blockIdx.x * P + p;
-        if (sr.seg > 0) prev = mine - per_seg;
+        ipos = sr.seg * per_seg + (size_t)blockIdx.x * P + p;
+        npos = (size_t)sg.G * per_seg;
+        mine = reinterpret_cast<SmaSegRec*>(sg.rec) + ipos;
         if (fix_seg > 0) {  // re-walk only if some lane started in a position other than the true one
-            if (!__syncthreads_or(active && mine->start_pos != prev->end_pos)) return;
+            // (the int8 planes: 2 B per lane instead of a line of each record)
+            if (!__syncthreads_or(active && sg.pos[ipos] != sg.pos[npos + ipos - per_seg])) return;
             if (tid == 0) atomicAdd(sg.refixed, 1ULL);
         }
     }
@@ -524,7 +526,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     a.carried = a.x1 = a.px1 = 0;
     a.agg1 = kAggId;
     int32_t start_pos = 0;
-    if (SEG && fix_seg > 0 && active) a.pos = prev->end_pos;  // the true position entering
+    // the true position entering (the previous segment's end)
+    if (SEG && fix_seg > 0 && active) a.pos = sg.pos[npos + ipos - (size_t)gridDim.x * P];
     // SEG: at the first accounted bar keep the position, drop the burn-in's accounts, and carry
     // the open trade (its entry lies before the segment) symbolically from here
     auto enter_acct = [&]() {
@@ -756,16 +759,17 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             r.end_agg[2] = a.agg.dd;
             r.end_agg[3] = a.agg.du;
             r.R = a.R;
-            r.A = -a.R;
             r.B = a.Bq;
             r.C = a.C;
             r.D = a.D;
             r.h = a.h;
             r.s1lo = a.s1.lo;
-            r.s1hi = a.s1.hi64();
+            r.s1hi = a.s1.hi;
             r.s2lo = a.s2.lo;
-            r.s2hi = a.s2.hi64();
+            r.s2hi = a.s2.hi;
             *mine = r;
+            sg.pos[ipos] = (int8_t)start_pos;
+            sg.pos[npos + ipos] = (int8_t)a.pos;
         }
         return;
     }
@@ -827,8 +831,8 @@ __global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict
             ntr += r.ntr;
             R += r.R;
             h += r.h;
-            s1 += (i128)(((unsigned __int128)(uint64_t)r.s1hi << 64) | r.s1lo);
-            s2 += (i128)(((unsigned __int128)(uint64_t)r.s2hi << 64) | r.s2lo);
+            s1 += (i128)(((unsigned __int128)(uint64_t)(int64_t)r.s1hi << 64) | r.s1lo);
+            s2 += (i128)(((unsigned __int128)(uint64_t)(int64_t)r.s2hi << 64) | r.s2lo);
             if (e0 < 0) e0 = r.e0;
             const Agg a1 = Agg{r.agg1[0], r.agg1[1], r.agg1[2], r.agg1[3]};
             if (pos != 0) {
@@ -849,7 +853,7 @@ __global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict
                 }
             }
             mdd = max(mdd, max(gap + r.C, r.D));
-            gap = max(gap + r.A, r.B);
+            gap = max(gap - r.R, r.B);  // A = -R
             if (r.end_pos == 0) {
                 pos = 0;
             } else if (r.end_e >= 0) {  // a trade opened in this segment is open at its end

@@ -1150,13 +1150,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         XL = (int32_t)yl;
         XHm1 = yh >= 2147483648.0 ? INT32_MAX : (int32_t)yh - 1;
     };
-    int32_t start_pos = 0, start_e = 0;  // SEG: state at the first accounted bar
+    // SEG: this lane's record; the state at the first accounted bar goes there when the walk
+    // reaches it (seg_write_start), the rest at the end. The address is recomputed at both
+    // points from an opaque copy of the parameter index (kept live, a pointer costs a VGPR pair)
+    auto seg_rec = [&]() {
+        int pje = pj;
+        asm volatile("" : "+v"(pje));
+        return sg.rec + (size_t)sr.seg * gridDim.x * P + (size_t)blockIdx.x * P + pje;
+    };
     if (SEG && fix_seg > 0 && active) {  // the true state entering the segment
         seg_inject(a, prev);
         if (a.pos != 0) set_levels(a.ce, a.pos);
         fpos = a.pos;
-        start_pos = a.pos;
-        start_e = a.e;
     }
     const size_t gi = (size_t)blockIdx.x * P + pj;
     bt_trade* tr = (PARITY && keeps) ? out.trades + gi * out.trade_cap : nullptr;
@@ -1195,8 +1200,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         if (SEG && ka == T_acct && keeps) {
             // first accounted tile: keep the state the (speculative) walk reached, drop the
             // burn-in's sums (a trade open here is closed and accounted in this segment)
-            start_pos = a.pos;
-            start_e = a.e;
+            seg_write_start(seg_rec(), a.pos, a.e);
             seg_reset_sums(a);
         }
         if (walks && k >= T_walk && k < T_end && !BT_ABL(g, 8)) {
@@ -1450,11 +1454,12 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     if (STAMPS && blockIdx.x == 0 && blockIdx.z == 0 && lane == 0 && hw_wave < 8 && out.dbg != nullptr)
         out.dbg[56 + hw_wave] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) + 1;
     if (SEG) {
-        // the record's address again (keeping `mine` live across the whole walk costs a VGPR pair
-        // at the 128-register edge)
-        int pje = pj;
-        asm volatile("" : "+v"(pje));  // opaque: the address is not merged with `mine`
-        if (keeps) seg_write(a, start_pos, start_e, sg.rec + (size_t)sr.seg * gridDim.x * P + (size_t)blockIdx.x * P + pje);
+        if (keeps) {
+            // a segment with no bars never reached its first accounted tile: the state passes
+            // through (flat, or the fix pass's injected one)
+            if (T_acct >= T_end) seg_write_start(seg_rec(), a.pos, a.e);
+            seg_write_rest(a, seg_rec());
+        }
         return;
     }
     if (keeps) acct_write(a, B, g.sqrt_ann, (size_t)blockIdx.x * P + pj_out, out);

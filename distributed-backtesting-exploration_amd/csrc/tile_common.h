@@ -311,6 +311,40 @@ __device__ __forceinline__ void seg_reset_sums(TradeAcct& a) {
     a.ps1 = a.ps2 = 0;
 }
 
+// The state at the segment's first accounted bar, stored when the walk reaches it (the Bollinger
+// kernel keeps no register for it across the walk); seg_write_rest then leaves it in place.
+__device__ __forceinline__ void seg_write_start(SegRec* mine, int start_pos, int start_e) {
+    *reinterpret_cast<int2*>(&mine->start_pos) = make_int2(start_pos, start_e);
+}
+
+__device__ __forceinline__ void seg_write_rest(const TradeAcct& a, SegRec* mine) {
+    *reinterpret_cast<int2*>(&mine->ntr) = make_int2(a.ntr, a.expo);
+    SegRec r;
+    r.end_pos = a.pos;
+    r.end_e = a.e;
+    r.end_ce = a.ce;
+    r.pad = 0;
+    r.end_agg[0] = a.agg.mx;
+    r.end_agg[1] = a.agg.mn;
+    r.end_agg[2] = a.agg.dd;
+    r.end_agg[3] = a.agg.du;
+    r.R = a.R;
+    r.A = -a.R;
+    r.B = a.Bq;
+    r.C = a.C;
+    r.D = a.D;
+    r.h = a.h;
+    r.s1lo = a.s1.lo;
+    r.s1hi = a.s1.hi64();
+    r.s2lo = a.s2.lo;
+    r.s2hi = a.s2.hi64();
+    // bytes 16..127 of the record (16-B aligned: records are 128 B)
+    const int4* src = reinterpret_cast<const int4*>(&r) + 1;
+    int4* dst = reinterpret_cast<int4*>(mine) + 1;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) dst[i] = src[i];
+}
+
 __device__ __forceinline__ void seg_write(const TradeAcct& a, int start_pos, int start_e, SegRec* mine) {
     SegRec r;
     r.ntr = a.ntr;

@@ -18,3 +18,4 @@ for r in 1 2; do
 done
 LIBS="libbt_base.so libbt.so" CFG=4 SYMS="500" bash scripts/gpu_ab_libs.sh || exit 1
 LIBS="libbt_base.so libbt.so" CFG=2 SYMS="5000" bash scripts/gpu_ab_libs.sh || exit 1
+LIBS="libbt_base.so libbt.so libbt_base.so libbt.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1
