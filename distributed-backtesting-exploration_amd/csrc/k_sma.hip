@@ -38,6 +38,10 @@ constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned
 constexpr int kStages = 3;            // tile buffers in flight (cT, Q)
 constexpr int kDstStages = 2;         // drawdown tables: built in interval k - 1, read in k
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
+#ifndef BT_CMP_DEPTH1
+#define BT_CMP_DEPTH1 2
+#endif
+constexpr int kCmpDepth1 = BT_CMP_DEPTH1;  // key-row pairs in flight in a ONE_TRIP compare
 
 struct SmaLds {                       // byte offsets into dynamic LDS
     size_t ring, keys, invw, win, dst, ct, ql, nar, ctr, total;
@@ -613,8 +617,11 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
                 for (int v = 0; v < 16; ++v) {
                     if (v < 8) cmp4(l0, z, k1[v], k2[v]);
                     else cmp4(l1, z, k1[v], k2[v]);
-                    // keep the schedule to two int4 pairs in flight (VGPR budget)
-                    if (v & 1) __builtin_amdgcn_sched_barrier(0);
+                    // keep the schedule to two int4 pairs in flight at config 2's 80-VGPR budget;
+                    // a one-block-per-CU 16-wave block (ONE_TRIP, up to 128 VGPRs, 4 waves per
+                    // SIMD to hide LDS latency) keeps kCmpDepth1 pairs in flight
+                    if (ONE_TRIP ? ((v % kCmpDepth1) == kCmpDepth1 - 1) : (v & 1))
+                        __builtin_amdgcn_sched_barrier(0);
                 }
             }
             BT_STAMP(2)

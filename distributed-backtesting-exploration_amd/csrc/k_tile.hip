@@ -58,6 +58,18 @@ constexpr int kBollStages = 4;
 // Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
 // after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
 constexpr int kRecCap = 33;
+// EMA+OLS walk accounts in int32 while the closes' total variation allows (unsplit runs)
+#ifndef BT_EMA_NARROW
+#define BT_EMA_NARROW 1
+#endif
+constexpr bool kEmaNarrow = BT_EMA_NARROW;
+
+// bar segments' accountant in int32 while the segment's total variation allows (Acct32 SEG forms)
+#ifndef BT_BOLL_SEG_NARROW
+#define BT_BOLL_SEG_NARROW 0
+#endif
+constexpr bool kBollSegNarrow = BT_BOLL_SEG_NARROW;
+
 // Bollinger per-stage low/high staging (int32): lows[64], highs[64], 8 block minima of the lows
 // then 8 block maxima of the highs, per bar the minimum low / maximum high from that bar to the
 // end of its 8-bar block, and per bar the minimum low / maximum high from that bar to the end of
@@ -99,6 +111,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
         L.win = take((size_t)nb * 4);
+        L.nar = take((size_t)ns * 4);  // per tile stage: the walk's accounts fit int32 (Acct32)
     }
     L.ctr = take(4);
     L.total = o;
@@ -235,6 +248,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     double* ebuf = reinterpret_cast<double*>(smem + LL.ebuf);  // [2][nsp][kEStride]
     uint64_t* words = reinterpret_cast<uint64_t*>(smem + LL.words);
     int32_t* win = reinterpret_cast<int32_t*>(smem + LL.win);
+    int32_t* nars = reinterpret_cast<int32_t*>(smem + LL.nar);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -364,7 +378,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     auto scan = [&](int T, int32_t c) {
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
-                                      dst + s * kDstLevels * kTile, cy, !BT_ABL(g, 512));
+                                      dst + s * kDstLevels * kTile, cy, !BT_ABL(g, 512),
+                                      SEG ? nullptr : nars + s);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (uint64_t)pre;
         const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end
@@ -565,43 +580,60 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 }
                 const uint64_t Lb = (Lw << 1) | lin, Sb = (Sw << 1) | sin;
                 const uint64_t EL = Lw & ~Lb;
-                uint64_t Ev = EL | (Sw & ~Sb), Xv = (Lb & ~Lw) | (Sb & ~Sw);
-                if (a.pos != 0 && Xv) {  // the position carried in closes first
-                    const int x = __builtin_ctzll(Xv);
-                    Xv &= Xv - 1;
-                    const int32_t cx = cT[x];
-                    const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                    const bool lg = a.pos > 0;
-                    acct_close<PARITY, SEG>(a, t0 + x, cx, agg_merge(a.agg, dst_query_bf(D, a.sb, x)), tr, cap);
-                    a.ps1 += lg ? qx : (uint64_t)0 - qx;
-                    a.ps2 += q2x;
-                    a.pos = 0;
-                }
+                const uint64_t Ev0 = EL | (Sw & ~Sb), Xv0 = (Lb & ~Lw) | (Sb & ~Sw);
+                // the trades of the tile; NARROW: gap and mdd in int32 while the closes' total
+                // variation allows (tile_common.h Acct32; fills are at closes), one copy of the
+                // loop per width, chosen per tile (wave-uniform)
+                auto trades = [&](auto narrow_tag) {
+                    constexpr bool NARROW = decltype(narrow_tag)::value;
+                    Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd, 0, 0, 0};  // <= TV < 2^30 if NARROW
+                    uint64_t Ev = Ev0, Xv = Xv0;
+                    if (a.pos != 0 && Xv) {  // the position carried in closes first
+                        const int x = __builtin_ctzll(Xv);
+                        Xv &= Xv - 1;
+                        const int32_t cx = cT[x];
+                        const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                        const bool lg = a.pos > 0;
+                        acct_close<PARITY, SEG, NARROW>(a, n32, t0 + x, cx,
+                                                        agg_merge(a.agg, dst_query_bf(D, a.sb, x)), tr, cap);
+                        a.ps1 += lg ? qx : (uint64_t)0 - qx;
+                        a.ps2 += q2x;
+                        a.pos = 0;
+                    }
 #pragma unroll 1
-                while (Ev) {
-                    if (STAMPS) sa.count(3);
-                    // entry and exit bars are both known: every LDS read of the trade is issued
-                    // together (an entry left open reads the tile's last bar, unused)
-                    const int b = __builtin_ctzll(Ev);
-                    Ev &= Ev - 1;
-                    const bool hx = Xv != 0;
-                    const int x = hx ? __builtin_ctzll(Xv) : kTile - 1;
-                    Xv &= Xv - 1;
-                    const int32_t cb = cT[b], cx = cT[x];
-                    const uint64_t qb = (uint64_t)ql[b], q2b = (uint64_t)ql[kTile + b];
-                    const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                    const Agg st = dst_query_bf(D, b, x);
-                    const int np = ((EL >> b) & 1) ? 1 : -1;
-                    a.ps1 += np > 0 ? (uint64_t)0 - qb : qb;
-                    a.ps2 -= q2b;
-                    acct_open(a, t0 + b, b, cb);
-                    a.pos = np;
-                    if (!hx) break;  // open at the tile end
-                    acct_close<PARITY, SEG>(a, t0 + x, cx, st, tr, cap);
-                    a.ps1 += np > 0 ? qx : (uint64_t)0 - qx;
-                    a.ps2 += q2x;
-                    a.pos = 0;
-                }
+                    while (Ev) {
+                        if (STAMPS) sa.count(3);
+                        // entry and exit bars are both known: every LDS read of the trade is
+                        // issued together (an entry left open reads the tile's last bar, unused)
+                        const int b = __builtin_ctzll(Ev);
+                        Ev &= Ev - 1;
+                        const bool hx = Xv != 0;
+                        const int x = hx ? __builtin_ctzll(Xv) : kTile - 1;
+                        Xv &= Xv - 1;
+                        const int32_t cb = cT[b], cx = cT[x];
+                        const uint64_t qb = (uint64_t)ql[b], q2b = (uint64_t)ql[kTile + b];
+                        const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
+                        const Agg st = dst_query_bf(D, b, x);
+                        const int np = ((EL >> b) & 1) ? 1 : -1;
+                        a.ps1 += np > 0 ? (uint64_t)0 - qb : qb;
+                        a.ps2 -= q2b;
+                        acct_open(a, t0 + b, b, cb);
+                        a.pos = np;
+                        if (!hx) break;  // open at the tile end
+                        acct_close<PARITY, SEG, NARROW>(a, n32, t0 + x, cx, st, tr, cap);
+                        a.ps1 += np > 0 ? qx : (uint64_t)0 - qx;
+                        a.ps2 += q2x;
+                        a.pos = 0;
+                    }
+                    if (NARROW) {
+                        a.gap = (uint32_t)n32.g;  // >= 0
+                        a.mdd = (uint32_t)n32.m;
+                    }
+                };
+                if (!SEG && kEmaNarrow && __builtin_amdgcn_readfirstlane(nars[s]))
+                    trades(std::true_type{});
+                else
+                    trades(std::false_type{});
             }
             if (STAMPS) sa.mark(1);
             acct_tile_end(a, D, ql);
@@ -738,12 +770,6 @@ __device__ __forceinline__ double level_y(double ce, double g) { return ce * g +
 // boundary fix_seg: the block re-walks that segment from the previous segment's end states if
 // any lane's speculative start differs, and otherwise returns at once). Results go to SegRec
 // records (internal.h) that seg_combine folds.
-// bar segments' accountant in int32 while the segment's total variation allows (Acct32 SEG forms)
-#ifndef BT_BOLL_SEG_NARROW
-#define BT_BOLL_SEG_NARROW 0
-#endif
-constexpr bool kBollSegNarrow = BT_BOLL_SEG_NARROW;
-
 template <bool PARITY, bool STAMPS, bool SEG>
 __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restrict__ syms,
                                                          const int32_t* __restrict__ high,

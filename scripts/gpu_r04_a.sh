@@ -13,9 +13,7 @@ tail -2 gpurun_out/r04/pytest_gpu.log
 BT_LIB=libbt_sn.so timeout -k 10 300 $T tests/test_gpu_segments.py tests/test_gpu_shards.py tests/test_gpu_narrow.py -m gpu -k "boll or Boll or 4" > gpurun_out/r04/pytest_sn.log 2>&1 || { tail -30 gpurun_out/r04/pytest_sn.log; exit 1; }
 tail -1 gpurun_out/r04/pytest_sn.log
 for r in 1 2; do
-  LIBS="libbt_base.so libbt.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
+  LIBS="libbt_base.so libbt.so libbt_en0.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
   LIBS="libbt_base.so libbt.so libbt_sn.so" CFG=4 SYMS="250" bash scripts/gpu_ab_libs.sh || exit 1
 done
 LIBS="libbt_base.so libbt.so" CFG=4 SYMS="500" bash scripts/gpu_ab_libs.sh || exit 1
-LIBS="libbt_base.so libbt.so" CFG=2 SYMS="5000" bash scripts/gpu_ab_libs.sh || exit 1
-LIBS="libbt_base.so libbt.so libbt_base.so libbt.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1

@@ -206,3 +206,47 @@ def test_boll_narrow_to_wide_accounts_match_oracle(parity):
             compare_summary(got[s, p], orc[p], where)
             if parity:
                 compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
+EMA_BARS = 20_000
+
+
+def _ema_series():
+    """1-minute-like walks whose total variation crosses 2^30 at different tiles after the
+    config-3 grid's 1,560-bar warm-up, one narrow throughout and one wide from its first tile."""
+    rng = np.random.default_rng(31)
+    out = [_walk(rng, 1 << 28, step, bars=EMA_BARS) for step in (120_000, 160_000, 230_000, 400_000)]
+    out.append(_walk(rng, 5_000_000, 2_000, bars=EMA_BARS))           # TV ~ 2e7: narrow
+    out.append(_walk(rng, 1 << 30, 1 << 26, bars=EMA_BARS, lo=1 << 28))  # wide at once
+    return [x.astype(np.int32) for x in out]
+
+
+def test_ema_series_cross_the_narrow_bound_after_warm_up():
+    ks = [_first_wide_tile(c) for c in _ema_series()]
+    assert all(k is not None and 1560 // 64 < k < EMA_BARS // 64 - 1 for k in ks[:4]), ks
+    assert len(set(ks[:4])) == 4 and ks[4] is None and ks[5] == 0, ks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parity", [False, True])
+def test_ema_narrow_to_wide_accounts_match_oracle(parity):
+    """The EMA+OLS walk keeps gap and mdd in int32 while the closes' total variation is below
+    2^30 (k_tile.hip kEmaNarrow; fills are at closes, so the closes' TV bounds them), unsplit
+    runs only: every field and trade vs the C oracle across the crossing tiles."""
+    grid = D.config3_grid()
+    closes = _ema_series()
+    kw = dict(parity=True, trade_cap=CAP) if parity else {}
+    with D.Engine(grid, **kw) as e:
+        e.set_segments(1)
+        e.load_ohlc(closes)
+        e.run()
+        assert e.last_segments() == 1
+        got = e.summaries()
+        tr = e.trades() if parity else None
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("ema_ols", grid, (cl, cl, cl, cl), 98280, CAP if parity else 0)
+        for p in range(grid.n_params):
+            where = f"ema series {s} (first wide tile {_first_wide_tile(cl)}) {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            if parity:
+                compare_trades(tr[s, p], otr[p], min(int(orc[p]["n_trades"]), CAP), where)
