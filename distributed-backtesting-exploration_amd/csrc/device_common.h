@@ -12,6 +12,20 @@ __host__ __device__ inline uint64_t trade_mix(uint64_t w) {
     const uint64_t z = (w ^ (w >> 29)) * 0xBF58476D1CE4E5B9ULL;
     return z ^ (z >> 32);
 }
+// trade_mix of the one-word trade term w = e | t << 31 | side << 62 (spec §4) for bar indices
+// e, t < 2^22 (kMaxBars): w ^ (w >> 29) is formed in 32-bit halves with no 64-bit shift,
+//   lo = e ^ (t << 2) ^ (t << 31),  hi = (t >> 1) ^ (side ? 2^30 + 2 : 0)
+// (w >> 29 has lo = t << 2 and hi = side << 1 in that range; checked against trade_mix on 5e7
+// random terms, and bit for bit by every GPU parity test through the hash).
+__host__ __device__ inline uint64_t trade_mix_et(uint32_t e, uint32_t t, bool lg) {
+#if defined(BT_HASH_PLAIN)  // A/B aid: the generic form
+    return trade_mix((uint64_t)e | ((uint64_t)t << 31) | ((uint64_t)lg << 62));
+#endif
+    const uint32_t lo = e ^ (t << 2) ^ (t << 31);
+    const uint32_t hi = (t >> 1) ^ (lg ? 0x40000002u : 0u);
+    const uint64_t z = (((uint64_t)hi << 32) | lo) * 0xBF58476D1CE4E5B9ULL;
+    return z ^ (z >> 32);
+}
 constexpr int kDstLevels = 6;      // log2(kTile)
 constexpr int kKeyStride = kTile + 1;  // +1 double per key row: conflict-free ds_read_b64
 

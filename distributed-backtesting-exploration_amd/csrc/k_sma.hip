@@ -301,9 +301,7 @@ __device__ __forceinline__ void sma_close(SmaAcct& a, const Agg& seg, int t, int
         a.r32 += pnl;
     else
         a.R += pnl;
-    const uint64_t w = (uint64_t)(uint32_t)a.e | ((uint64_t)(uint32_t)t << 31) |
-                       ((uint64_t)lg << 62);
-    a.h += trade_mix(w);
+    a.h += trade_mix_et((uint32_t)a.e, (uint32_t)t, lg);
     if (PARITY && a.ntr < cap) {
         bt_trade r;
         r.entry_bar = a.e;

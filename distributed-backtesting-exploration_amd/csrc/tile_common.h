@@ -193,7 +193,7 @@ __device__ __forceinline__ void acct_fold(TradeAcct& a, Acct32& n, int t, int32_
 
 // Hash term of a trade (spec §4): w = entry | exit << 31 | (side > 0) << 62.
 __device__ __forceinline__ uint64_t trade_term(int e, int t, bool lg) {
-    return trade_mix((uint64_t)(uint32_t)e | ((uint64_t)(uint32_t)t << 31) | ((uint64_t)lg << 62));
+    return trade_mix_et((uint32_t)e, (uint32_t)t, lg);
 }
 
 // Close the open trade at global bar t for price px; `st` aggregates the trade's whole price

@@ -16,4 +16,4 @@ for r in 1 2; do
   LIBS="libbt_base.so libbt.so libbt_en0.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
   LIBS="libbt_base.so libbt.so libbt_sn.so" CFG=4 SYMS="250" bash scripts/gpu_ab_libs.sh || exit 1
 done
-LIBS="libbt_base.so libbt.so" CFG=4 SYMS="500" bash scripts/gpu_ab_libs.sh || exit 1
+LIBS="libbt_base.so libbt.so libbt_hp.so libbt.so libbt_hp.so" CFG=4 SYMS="500" bash scripts/gpu_ab_libs.sh || exit 1
