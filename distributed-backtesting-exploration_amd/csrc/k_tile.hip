@@ -58,6 +58,10 @@ constexpr int kBollStages = 4;
 // Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
 // after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
 constexpr int kRecCap = 33;
+#ifndef BT_CHAIN_OPAQUE
+#define BT_CHAIN_OPAQUE 0
+#endif
+
 // EMA+OLS walk accounts in int32 while the closes' total variation allows (unsplit runs)
 #ifndef BT_EMA_NARROW
 #define BT_EMA_NARROW 1
@@ -409,13 +413,19 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 for (int b = 0; b < kTile; ++b) E[b] = (double)__builtin_amdgcn_readlane(cl, b);
             } else if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
                 // 8 bars' closes read one chunk ahead (the reads precede, in program order, the
-                // chain's stores that may alias them). Both rows are addressed from opaque LDS
-                // pointers: with the buffer's constant offset folded into the addresses, every
-                // ds_write2/ds_read2 (8-bit offsets) needed its own v_add / v_mov
+                // chain's stores that may alias them). BT_CHAIN_OPAQUE addresses both rows from
+                // opaque LDS pointers (immediate offsets, no v_add / v_mov per ds_write2 /
+                // ds_read2): measured 6 % slower on config 3 (the compiler then cannot tell the
+                // rows apart and schedules the reads behind the stores), so off
+#if BT_CHAIN_OPAQUE
                 lds_f64* Ev = (lds_f64*)E;
                 const lds_f64* Cv = (const lds_f64*)CD;
                 asm volatile("" : "+v"(Ev));
                 asm volatile("" : "+v"(Cv));
+#else
+                double* Ev = E;
+                const double* Cv = CD;
+#endif
                 double nx[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) nx[u] = Cv[u];

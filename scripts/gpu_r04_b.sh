@@ -4,6 +4,7 @@
 # compare), then the diagnostics (stamps, per-dispatch HBM bytes of a config-5 step).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r04
 export PYTHONUNBUFFERED=1
+LIBS="libbt_base.so libbt.so libbt_co.so libbt_base.so libbt.so libbt_co.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
 LIBS="libbt_base.so libbt.so libbt_hp.so libbt_base.so libbt.so libbt_hp.so" CFG=2 SYMS="5000" bash scripts/gpu_ab_libs.sh || exit 1
 LIBS="libbt_base.so libbt.so libbt_c4.so libbt_c8.so libbt_c16.so libbt.so libbt_c4.so libbt_c8.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1
 bash scripts/gpu_r04_diag.sh
