@@ -39,15 +39,21 @@ constexpr int kStages = 3;            // tile buffers in flight (cT, Q)
 constexpr int kDstStages = 2;         // drawdown tables: built in interval k - 1, read in k
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
 #ifndef BT_CMP_DEPTH1
-#define BT_CMP_DEPTH1 2
+#define BT_CMP_DEPTH1 16
 #endif
 constexpr int kCmpDepth1 = BT_CMP_DEPTH1;  // key-row pairs in flight in a ONE_TRIP compare
-// Stage 1 as a task of the stage-2 round (any wave) instead of a fixed duty of the last wave:
-// always for blocks whose last wave also walks parameters (config 5's 16-wave blocks, where it
-// set the tile), and for every block with BT_S1TASK_ALL (A/B aid).
+// Stage 1 as a task of the stage-2 round (any wave) instead of a fixed duty of the last wave,
+// for blocks whose last wave also walks parameters (BT_S1TASK_16, config 5's 16-wave blocks) or
+// for every block (BT_S1TASK_ALL). Measured (round 4, interleaved A/B): config 5's shard
+// 137.6 -> 137.6-137.9 ms (neutral), config 2 1.16 -> 1.21 ms; both off by default.
+#ifndef BT_S1TASK_16
+#define BT_S1TASK_16 0
+#endif
 #ifndef BT_S1TASK_ALL
 #define BT_S1TASK_ALL 0
 #endif
+// Key-row pairs in flight in the 16-wave (ONE_TRIP) compare: 16 measured 137.0-137.2 vs
+// 137.6-137.9 ms at 2 on config 5's shard (4, 8: within noise of 2).
 
 struct SmaLds {                       // byte offsets into dynamic LDS
     size_t ring, keys, invw, win, dst, ct, ql, nar, stc, cyl, ctr, total;
@@ -516,18 +522,28 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     const uint32_t fsw = (uint32_t)win[kf] | ((uint32_t)win[ks] << 16);
 
     ScanCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
-    // SEG lookback: the prefix ring over the windows before the first walked bar (the next tile's
-    // closes in flight while one is summed)
+    // SEG lookback: the prefix ring over the windows before the first walked bar (config 5: 100
+    // tiles). The loop is bound by the load latency, so kLookAhead tiles' closes are in flight
+    // while one is summed (one in flight made the lookback ~5 % of a segment block)
     if (SEG && helper && T_scan < T_walk) {
-        int32_t cn = load_close(crow, B, T_scan * kTile + lane);
+        constexpr int kLookAhead = 8;
+        int32_t cn[kLookAhead];
+#pragma unroll
+        for (int u = 0; u < kLookAhead; ++u) cn[u] = load_close(crow, B, (T_scan + u) * kTile + lane);
 #pragma unroll 1
-        for (int T = T_scan; T < T_walk; ++T) {
-            const int32_t c = cn;
-            cn = load_close(crow, B, (T + 1) * kTile + lane);
-            const int64_t inc = wave_iscan_i64((int64_t)c);
-            ring[(T * kTile + lane + 1) & (R - 1)] = (double)(cy.P + inc);
-            cy.P += lane63_i64(inc);
-            cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
+        for (int T0 = T_scan; T0 < T_walk; T0 += kLookAhead) {
+#pragma unroll
+            for (int u = 0; u < kLookAhead; ++u) {
+                const int T = T0 + u;
+                if (T < T_walk) {  // wave-uniform
+                    const int32_t c = cn[u];
+                    cn[u] = load_close(crow, B, (T + kLookAhead) * kTile + lane);
+                    const int64_t inc = wave_iscan_i64((int64_t)c);
+                    ring[(T * kTile + lane + 1) & (R - 1)] = (double)(cy.P + inc);
+                    cy.P += lane63_i64(inc);
+                    cy.prevc = (int32_t)__builtin_amdgcn_readlane((uint32_t)c, 63);
+                }
+            }
         }
     }
     // prologue: stage 1 for the first two walked tiles; stage 2 for the first. The helper keeps
@@ -852,11 +868,20 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
-template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool S1>
+// Blocks of up to 8 waves: six waves per SIMD (three blocks per CU) need <= 80 VGPRs.
+template <bool PARITY, bool STAMPS, bool S1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(
     const SymDesc* __restrict__ syms, const int32_t* __restrict__ close, Grid g, Out out,
     int dedicated) {
-    sma_body<PARITY, STAMPS, ONE_TRIP, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
+    sma_body<PARITY, STAMPS, false, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
+}
+
+// Blocks of more than 8 waves (ONE_TRIP) run one per CU: up to 128 VGPRs.
+template <bool PARITY, bool S1>
+__global__ __launch_bounds__(1024) void sma_kernel_wide(const SymDesc* __restrict__ syms,
+                                                        const int32_t* __restrict__ close, Grid g,
+                                                        Out out, int dedicated) {
+    sma_body<PARITY, false, true, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
 }
 
 // Bar segments (SMA_SEG): its own kernel, for one-block-per-CU shapes (up to 128 VGPRs).
@@ -999,12 +1024,15 @@ hipError_t launch_sma_variant(const SymDesc* syms, int32_t n_sym, const int32_t*
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(sma_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym,
                            g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec), seg.G, g.sqrt_ann, out);
+    } else if (ONE_TRIP) {
+        if (parity)
+            hipLaunchKernelGGL((sma_kernel_wide<true, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        else
+            hipLaunchKernelGGL((sma_kernel_wide<false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     } else if (parity) {
-        hipLaunchKernelGGL((sma_kernel<true, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
-                           sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<true, false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     } else {
-        hipLaunchKernelGGL((sma_kernel<false, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
-                           sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<false, false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     }
     return hipGetLastError();
 }
@@ -1025,16 +1053,16 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     if (BT_ABL(g, 64)) {
         const dim3 grid(n_sym, sh.gy), block(sh.block);
         if (sh.dedicated)
-            hipLaunchKernelGGL((sma_kernel<false, true, false, BT_S1TASK_ALL != 0>), grid, block, lds, st, syms,
+            hipLaunchKernelGGL((sma_kernel<false, true, BT_S1TASK_ALL != 0>), grid, block, lds, st, syms,
                                close, g, out, sh.dedicated);
         else
-            hipLaunchKernelGGL((sma_kernel<false, true, false, true>), grid, block, lds, st, syms, close, g, out,
-                               sh.dedicated);
+            hipLaunchKernelGGL((sma_kernel<false, true, BT_S1TASK_16 != 0>), grid, block, lds, st, syms, close,
+                               g, out, sh.dedicated);
         return hipGetLastError();
     }
 #endif
     // stage 1 as a stage-2 task when the last wave also walks parameters (no dedicated helper)
-    const bool s1 = !sh.dedicated || BT_S1TASK_ALL;
+    const bool s1 = (!sh.dedicated && BT_S1TASK_16) || BT_S1TASK_ALL;
     if (one_trip && s1) return launch_sma_variant<true, true>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
     if (one_trip) return launch_sma_variant<true, false>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
     if (s1) return launch_sma_variant<false, true>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
