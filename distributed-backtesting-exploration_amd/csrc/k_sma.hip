@@ -39,7 +39,7 @@ constexpr int kStages = 3;            // tile buffers in flight (cT, Q)
 constexpr int kDstStages = 2;         // drawdown tables: built in interval k - 1, read in k
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
 #ifndef BT_CMP_DEPTH1
-#define BT_CMP_DEPTH1 16
+#define BT_CMP_DEPTH1 2
 #endif
 constexpr int kCmpDepth1 = BT_CMP_DEPTH1;  // key-row pairs in flight in a ONE_TRIP compare
 // Stage 1 as a task of the stage-2 round (any wave) instead of a fixed duty of the last wave,
@@ -52,8 +52,9 @@ constexpr int kCmpDepth1 = BT_CMP_DEPTH1;  // key-row pairs in flight in a ONE_T
 #ifndef BT_S1TASK_ALL
 #define BT_S1TASK_ALL 0
 #endif
-// Key-row pairs in flight in the 16-wave (ONE_TRIP) compare: 16 measured 137.0-137.2 vs
-// 137.6-137.9 ms at 2 on config 5's shard (4, 8: within noise of 2).
+// Key-row pairs in flight in the 16-wave (ONE_TRIP) compare: 2, 4, 8 and 16 are within 0.5 %
+// of each other on config 5's shard (round 4); the whole 10,000-symbol workload ran 3 % slower
+// with 16 and no VGPR cap, so 2.
 
 struct SmaLds {                       // byte offsets into dynamic LDS
     size_t ring, keys, invw, win, dst, ct, ql, nar, stc, cyl, ctr, total;
@@ -868,20 +869,11 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
-// Blocks of up to 8 waves: six waves per SIMD (three blocks per CU) need <= 80 VGPRs.
-template <bool PARITY, bool STAMPS, bool S1>
+template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool S1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(
     const SymDesc* __restrict__ syms, const int32_t* __restrict__ close, Grid g, Out out,
     int dedicated) {
-    sma_body<PARITY, STAMPS, false, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
-}
-
-// Blocks of more than 8 waves (ONE_TRIP) run one per CU: up to 128 VGPRs.
-template <bool PARITY, bool S1>
-__global__ __launch_bounds__(1024) void sma_kernel_wide(const SymDesc* __restrict__ syms,
-                                                        const int32_t* __restrict__ close, Grid g,
-                                                        Out out, int dedicated) {
-    sma_body<PARITY, false, true, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
+    sma_body<PARITY, STAMPS, ONE_TRIP, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
 }
 
 // Bar segments (SMA_SEG): its own kernel, for one-block-per-CU shapes (up to 128 VGPRs).
@@ -1024,15 +1016,12 @@ hipError_t launch_sma_variant(const SymDesc* syms, int32_t n_sym, const int32_t*
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(sma_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym,
                            g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec), seg.G, g.sqrt_ann, out);
-    } else if (ONE_TRIP) {
-        if (parity)
-            hipLaunchKernelGGL((sma_kernel_wide<true, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
-        else
-            hipLaunchKernelGGL((sma_kernel_wide<false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
     } else if (parity) {
-        hipLaunchKernelGGL((sma_kernel<true, false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<true, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
+                           sh.dedicated);
     } else {
-        hipLaunchKernelGGL((sma_kernel<false, false, S1>), grid, block, lds, st, syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<false, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
+                           sh.dedicated);
     }
     return hipGetLastError();
 }
@@ -1053,11 +1042,11 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     if (BT_ABL(g, 64)) {
         const dim3 grid(n_sym, sh.gy), block(sh.block);
         if (sh.dedicated)
-            hipLaunchKernelGGL((sma_kernel<false, true, BT_S1TASK_ALL != 0>), grid, block, lds, st, syms,
-                               close, g, out, sh.dedicated);
+            hipLaunchKernelGGL((sma_kernel<false, true, false, BT_S1TASK_ALL != 0>), grid, block, lds, st,
+                               syms, close, g, out, sh.dedicated);
         else
-            hipLaunchKernelGGL((sma_kernel<false, true, BT_S1TASK_16 != 0>), grid, block, lds, st, syms, close,
-                               g, out, sh.dedicated);
+            hipLaunchKernelGGL((sma_kernel<false, true, false, BT_S1TASK_16 != 0>), grid, block, lds, st,
+                               syms, close, g, out, sh.dedicated);
         return hipGetLastError();
     }
 #endif

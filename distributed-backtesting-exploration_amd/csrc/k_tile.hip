@@ -67,6 +67,9 @@ constexpr int kRecCap = 33;
 #define BT_EMA_NARROW 1
 #endif
 constexpr bool kEmaNarrow = BT_EMA_NARROW;
+#ifndef BT_EMA_NAR_LDS
+#define BT_EMA_NAR_LDS 1
+#endif
 
 // bar segments' accountant in int32 while the segment's total variation allows (Acct32 SEG forms)
 #ifndef BT_BOLL_SEG_NARROW
@@ -115,7 +118,9 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
         L.win = take((size_t)nb * 4);
+#if BT_EMA_NAR_LDS
         L.nar = take((size_t)ns * 4);  // per tile stage: the walk's accounts fit int32 (Acct32)
+#endif
     }
     L.ctr = take(4);
     L.total = o;
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + s * kDstLevels * kTile, cy, !BT_ABL(g, 512),
-                                      SEG ? nullptr : nars + s);
+                                      (SEG || !kEmaNarrow) ? nullptr : nars + s);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (uint64_t)pre;
         const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end

@@ -110,7 +110,19 @@ struct I96 {
         lo = n;
     }
     __device__ __forceinline__ int64_t hi64() const { return (int64_t)hi; }
+    __device__ __forceinline__ uint64_t lo64() const { return lo; }
 };
+// The same interface over a full int128 (A/B aid for the tile kernels: BT_ACC_I128)
+struct I128Acc {
+    i128 v;
+    __device__ __forceinline__ void clear() { v = 0; }
+    __device__ __forceinline__ uint64_t lo64() const { return (uint64_t)v; }
+    __device__ __forceinline__ void add(int64_t x) { v += (i128)x; }
+    __device__ __forceinline__ int64_t hi64() const { return (int64_t)(v >> 64); }
+};
+#ifndef BT_ACC_I128
+#define BT_ACC_I128 0
+#endif
 
 
 struct TradeAcct {
@@ -118,7 +130,11 @@ struct TradeAcct {
     int64_t R, gap, mdd;
     int64_t Bq, C, D;                   // SEG walks only (A = -R)
     uint64_t ps1, ps2, h;
+#if BT_ACC_I128
+    I128Acc s1, s2;
+#else
     I96 s1, s2;
+#endif
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
 };
 
@@ -239,7 +255,7 @@ __device__ __forceinline__ void acct_tile_end(TradeAcct& a, const Agg* D, const 
 
 __device__ __forceinline__ void acct_write(const TradeAcct& a, int bars, double sqrt_ann,
                                            size_t gi, const Out& out) {
-    const uint64_t s1lo = a.s1.lo, s2lo = a.s2.lo;
+    const uint64_t s1lo = a.s1.lo64(), s2lo = a.s2.lo64();
     const int64_t s1hi = a.s1.hi64(), s2hi = a.s2.hi64();
     const double sh = sharpe_fx(s1lo, s1hi, s2lo, s2hi, bars, sqrt_ann);
     bt_summary r;
@@ -334,9 +350,9 @@ __device__ __forceinline__ void seg_write_rest(const TradeAcct& a, SegRec* mine)
     r.C = a.C;
     r.D = a.D;
     r.h = a.h;
-    r.s1lo = a.s1.lo;
+    r.s1lo = a.s1.lo64();
     r.s1hi = a.s1.hi64();
-    r.s2lo = a.s2.lo;
+    r.s2lo = a.s2.lo64();
     r.s2hi = a.s2.hi64();
     // bytes 16..127 of the record (16-B aligned: records are 128 B)
     const int4* src = reinterpret_cast<const int4*>(&r) + 1;
@@ -365,9 +381,9 @@ __device__ __forceinline__ void seg_write(const TradeAcct& a, int start_pos, int
     r.C = a.C;
     r.D = a.D;
     r.h = a.h;
-    r.s1lo = a.s1.lo;
+    r.s1lo = a.s1.lo64();
     r.s1hi = a.s1.hi64();
-    r.s2lo = a.s2.lo;
+    r.s2lo = a.s2.lo64();
     r.s2hi = a.s2.hi64();
     *mine = r;
 }

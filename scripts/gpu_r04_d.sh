@@ -10,3 +10,6 @@ for r in 1 2; do
   LIBS="libbt_base.so libbt.so libbt_c2.so libbt_s16.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1
 done
 LIBS="libbt_base.so libbt.so" CFG=5 SYMS="10000" bash scripts/gpu_ab_libs.sh || exit 1
+for r in 1 2; do
+  LIBS="libbt_base.so libbt.so libbt_i128.so libbt_hp.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
+done
