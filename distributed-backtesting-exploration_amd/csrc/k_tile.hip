@@ -61,6 +61,9 @@ constexpr int kRecCap = 33;
 #ifndef BT_CHAIN_OPAQUE
 #define BT_CHAIN_OPAQUE 0
 #endif
+#ifndef BT_CHAIN_SB
+#define BT_CHAIN_SB 0
+#endif
 
 // EMA+OLS walk accounts in int32 while the closes' total variation allows (unsplit runs)
 #ifndef BT_EMA_NARROW
@@ -447,6 +450,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     for (int u = 0; u < 8; ++u) {
                         ema = ema + alpha * (cur[u] - ema);
                         Ev[8 * c + u] = ema;
+#if BT_CHAIN_SB
+                        if (u & 1) __builtin_amdgcn_sched_barrier(0);  // store each pair at once
+#endif
                     }
                 }
             } else {
@@ -610,7 +616,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                         const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
                         const bool lg = a.pos > 0;
                         acct_close<PARITY, SEG, NARROW>(a, n32, t0 + x, cx,
-                                                        agg_merge(a.agg, dst_query_bf(D, a.sb, x)), tr, cap);
+                                                        agg_merge(a.agg, dst_query_w(D, a.sb, x)), tr, cap);
                         a.ps1 += lg ? qx : (uint64_t)0 - qx;
                         a.ps2 += q2x;
                         a.pos = 0;
@@ -628,7 +634,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                         const int32_t cb = cT[b], cx = cT[x];
                         const uint64_t qb = (uint64_t)ql[b], q2b = (uint64_t)ql[kTile + b];
                         const uint64_t qx = (uint64_t)ql[x], q2x = (uint64_t)ql[kTile + x];
-                        const Agg st = dst_query_bf(D, b, x);
+                        // whole 16-B entries, kept live: the side's drawdown or draw-up is then
+                        // not re-read in a divergent branch (the compiler sank those reads once
+                        // the accounting changed shape: config 3 +2 %)
+                        const Agg st = dst_query_w(D, b, x);
                         const int np = ((EL >> b) & 1) ? 1 : -1;
                         a.ps1 += np > 0 ? (uint64_t)0 - qb : qb;
                         a.ps2 -= q2b;
