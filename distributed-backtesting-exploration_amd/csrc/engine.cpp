@@ -385,11 +385,10 @@ void run_impl(bt_engine* e) {
                                       : sma_auto_segments(S, e->P, maxb, e->grid.wmax, sg.burn_tiles);
             }
             if (sg.G > 1) {
-                // the SmaSegRec records (120 B), then the int8 start / end position planes
+                // one SegRec slot per SmaSegRec, then the int8 start / end position planes
                 const size_t nrec = (size_t)sg.G * S * e->P;
-                const size_t rec_bytes = nrec * sizeof(SmaSegRec);
-                e->d_seg.ensure((rec_bytes + 2 * nrec + sizeof(SegRec) - 1) / sizeof(SegRec));
-                sg.pos = reinterpret_cast<int8_t*>(e->d_seg.p) + rec_bytes;
+                e->d_seg.ensure(nrec + (2 * nrec + sizeof(SegRec) - 1) / sizeof(SegRec));
+                sg.pos = reinterpret_cast<int8_t*>(e->d_seg.p + nrec);
                 e->d_refixed.ensure(1);
                 HIPCHK(hipMemsetAsync(e->d_refixed.p, 0, sizeof(unsigned long long), e->stream));
                 sg.rec = e->d_seg.p;

@@ -89,24 +89,25 @@ static_assert(sizeof(SegRec) == 128, "SegRec layout");
 // for thousands of bars, so a segment cannot burn in to the entry of the trade open at its start.
 // That trade is carried symbolically: the segment records where and at what price it closes
 // and its path from the segment start, and the combine pass, which knows the entry from the
-// earlier segments, closes it. 120 B per (segment, symbol, param), written whole by its lane; the
-// positions entering and leaving the segment are in SegArgs::pos, the drawdown form A is -R (not
+// earlier segments, closes it. One 128-B line per (segment, symbol, param), written whole by its
+// lane (a full-line store; the combine reads it back once). The drawdown form A is -R (not
 // stored) and the Sharpe sums' high words fit int32 (|S| < 2^78, spec §3).
 struct SmaSegRec {
     int32_t ntr;                   // trades closed in the segment (the carried one included)
     int32_t e0;                    // first entry from flat in the segment (-1: none)
+    int32_t start_pos, end_pos;    // position entering the first accounted bar / after the last
     int32_t end_e, end_ce;         // trade open at the end, opened in the segment (end_e = -1:
                                    // the carried trade is still open: entry unknown here)
     int32_t x1, px1;               // the carried trade's exit bar (-1: still open) and fill
-    int32_t s1hi, s2hi;
     int32_t agg1[4];               // its path from the segment start to x1 (or to the end)
     int32_t end_agg[4];            // path of the trade open at the end, from its entry
     int64_t R;                     // pnl of the other trades closed in the segment (A = -R)
     int64_t B, C, D;               // their drawdown forms (SegRec)
     uint64_t h;                    // their additive hash
     uint64_t s1lo, s2lo;
+    int32_t s1hi, s2hi;
 };
-static_assert(sizeof(SmaSegRec) == 120, "SmaSegRec layout");
+static_assert(sizeof(SmaSegRec) == sizeof(SegRec), "SmaSegRec is one 128-B SegRec slot");
 struct SegArgs {
     SegRec* rec;
     // SMA: the positions entering and leaving every (segment, symbol, param), int8 planes

@@ -818,6 +818,8 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             SmaSegRec r;
             r.ntr = a.ntr;
             r.e0 = a.e0;
+            r.start_pos = start_pos;
+            r.end_pos = a.pos;
             r.end_e = a.carried ? -1 : a.e;
             r.end_ce = a.ce;
             r.x1 = a.x1;
@@ -886,18 +888,18 @@ __global__ __launch_bounds__(1024) void sma_seg_kernel(const SymDesc* __restrict
 // Folds the segments of every (symbol, param) in order (internal.h SmaSegRec): the trade open
 // across a boundary is closed here, with its entry from the segment that opened it and its path
 // merged over the segments it spans; the other trades' sums add and their drawdown forms compose.
-// The block's 256 records of a segment are read as one contiguous 30 KB run, 8 B per lane and
-// load (a streaming read, instead of loads per lane strided by the 120-B record), through LDS.
+// The block's 256 records of a segment are read as one contiguous 32 KB run, 16 B per lane and
+// load (a streaming read, instead of eight 16-B loads per lane strided by the 128-B record),
+// through LDS.
 __global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict__ syms, int n_sym,
                                                        int P, const SmaSegRec* __restrict__ rec,
-                                                       const int8_t* __restrict__ pos_end, int G,
-                                                       double sqrt_ann, Out out) {
-    __shared__ int2 stage[256 * sizeof(SmaSegRec) / sizeof(int2)];
+                                                       int G, double sqrt_ann, Out out) {
+    __shared__ int4 stage[256 * sizeof(SmaSegRec) / sizeof(int4)];
     const size_t i0 = (size_t)blockIdx.x * blockDim.x;
     const size_t i = i0 + threadIdx.x;
     const size_t n = (size_t)n_sym * P;
     const size_t nb = min((size_t)blockDim.x, n - i0);  // records of this block (per segment)
-    constexpr int kPer = sizeof(SmaSegRec) / sizeof(int2);  // 8-B chunks per record
+    constexpr int kPer = sizeof(SmaSegRec) / sizeof(int4);  // 16-B chunks per record
     int ntr = 0;
     {
         const int s = i < n ? (int)(i / P) : 0;
@@ -908,7 +910,7 @@ __global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict
         i128 s1 = 0, s2 = 0;
         for (int q = 0; q < G; ++q) {
             __syncthreads();  // the previous segment's records are consumed
-            const int2* src = reinterpret_cast<const int2*>(rec + (size_t)q * n + i0);
+            const int4* src = reinterpret_cast<const int4*>(rec + (size_t)q * n + i0);
             for (int c = threadIdx.x; c < (int)nb * kPer; c += blockDim.x) stage[c] = src[c];
             __syncthreads();
             if (i >= n) continue;
@@ -938,11 +940,10 @@ __global__ __launch_bounds__(256) void sma_seg_combine(const SymDesc* __restrict
             }
             mdd = max(mdd, max(gap + r.C, r.D));
             gap = max(gap - r.R, r.B);  // A = -R
-            const int end_pos = pos_end[(size_t)q * n + i];
-            if (end_pos == 0) {
+            if (r.end_pos == 0) {
                 pos = 0;
             } else if (r.end_e >= 0) {  // a trade opened in this segment is open at its end
-                pos = end_pos;
+                pos = r.end_pos;
                 e = r.end_e;
                 ce = r.end_ce;
                 agg = Agg{r.end_agg[0], r.end_agg[1], r.end_agg[2], r.end_agg[3]};
@@ -1002,9 +1003,12 @@ int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
     if (n_sym <= 0) return 1;
     const SmaShape sh = sma_shape(n_params);
     if (sh.block <= 512) return 1;
+    // enough segment blocks for ~kSegRounds rounds of one block per CU (config 5's 1,250-symbol
+    // shard, 4.9 rounds unsplit, round 4: G = 3 / 4 / 5 -> 135.0 / 133.5 / 132.4 ms)
+    constexpr double kSegRounds = 24.0;
     const double rounds = (double)n_sym * sh.gy / device_cus();
-    if (rounds >= 16.0) return 1;
-    int G = std::min(4, (int)std::ceil(16.0 / rounds));
+    if (rounds >= kSegRounds) return 1;
+    int G = std::min(8, (int)std::ceil(kSegRounds / rounds));
     const int ntiles = (max_bars + kTile - 1) / kTile;
     const int lookback = (wmax - 1 + kTile - 1) / kTile;
     while (G > 1 && burn_tiles + 0.05 * lookback > 0.02 * ntiles / G) --G;
@@ -1027,8 +1031,7 @@ hipError_t launch_sma_variant(const SymDesc* syms, int32_t n_sym, const int32_t*
                                close, g, out, sh.dedicated, seg, s);
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(sma_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym,
-                           g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec),
-                           seg.pos + (size_t)seg.G * n_sym * g.n_params, seg.G, g.sqrt_ann, out);
+                           g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec), seg.G, g.sqrt_ann, out);
     } else if (parity) {
         hipLaunchKernelGGL((sma_kernel<true, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
                            sh.dedicated);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4: 120-B SMA segment records (SMA segment / full-size tests), segment counts for config
-# 5's shard, and the config-3 LDS-layout hypothesis (libbt_en0l = EMA narrow off, no flag LDS).
+# 5's shard (automatic count: 5), base vs HEAD on that shard.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r04
 export PYTHONUNBUFFERED=1
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
@@ -10,6 +10,4 @@ for G in 4 5 6 8; do
   timeout -k 10 200 python3 bench.py --config 5 --symbols 1250 --segments $G --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r04/c5_G$G.log 2>&1 || { tail -5 gpurun_out/r04/c5_G$G.log; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/r04/c5_G$G.log').read().strip().splitlines()[-1]); print('config 5 1250 G', $G, 'kernel', round(d['roofline']['kernel_avg_ms'],3))"
 done
-for r in 1 2; do
-  LIBS="libbt_base.so libbt.so libbt_en0l.so" CFG=3 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
-done
+LIBS="libbt_base.so libbt.so libbt_base.so libbt.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1
