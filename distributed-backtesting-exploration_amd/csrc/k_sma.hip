@@ -1004,8 +1004,9 @@ int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
     const SmaShape sh = sma_shape(n_params);
     if (sh.block <= 512) return 1;
     // enough segment blocks for ~kSegRounds rounds of one block per CU (config 5's 1,250-symbol
-    // shard, 4.9 rounds unsplit, round 4: G = 3 / 4 / 5 -> 135.0 / 133.5 / 132.4 ms)
-    constexpr double kSegRounds = 24.0;
+    // shard, 4.9 rounds unsplit, round 4: G = 3 / 4 / 5 / 6 / 8 -> 135.0 / 133.5-134.0 /
+    // 132.4-132.5 / 132.0 / 132.5 ms; each segment adds one 128-B record per parameter)
+    constexpr double kSegRounds = 28.0;
     const double rounds = (double)n_sym * sh.gy / device_cus();
     if (rounds >= kSegRounds) return 1;
     int G = std::min(8, (int)std::ceil(kSegRounds / rounds));
