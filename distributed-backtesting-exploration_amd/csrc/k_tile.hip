@@ -80,6 +80,13 @@ constexpr bool kEmaNarrow = BT_EMA_NARROW;
 #endif
 constexpr bool kBollSegNarrow = BT_BOLL_SEG_NARROW;
 
+// the Bollinger walkers' (unsplit parameter waves') gap / mdd in int32 while the closes' total
+// variation allows (unsplit runs; tile_common.h acct_close_rt)
+#ifndef BT_BOLL_WALK_NARROW
+#define BT_BOLL_WALK_NARROW 1
+#endif
+constexpr bool kBollWalkNarrow = BT_BOLL_WALK_NARROW;
+
 // Bollinger per-stage low/high staging (int32): lows[64], highs[64], 8 block minima of the lows
 // then 8 block maxima of the highs, per bar the minimum low / maximum high from that bar to the
 // end of its 8-bar block, and per bar the minimum low / maximum high from that bar to the end of
@@ -1274,6 +1281,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int32_t* PH = PL + nlev * kTile;
             if (!finder) {
                 int cur = 0;
+                // gap / mdd in int32 this tile (unsplit runs; acct_close_rt)
+                const bool nar = !SEG && kBollWalkNarrow && __builtin_amdgcn_readfirstlane(nars[s]);
                 // walker: one trade (entry and/or exit) per call, in bar order; false when the
                 // tile is done. Only the first trade of the tile can start open (path carried in
                 // a.agg). Two LDS round trips per trade: everything the entry bar decides (close,
@@ -1338,7 +1347,10 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     const int32_t px = hit ? (low ? XL : XHm1 + 1) : cxx;
                     const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
                     const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
-                    acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
+                    if (SEG || !kBollWalkNarrow)
+                        acct_close<PARITY, SEG>(a, t0 + x, px, st, tr, cap);
+                    else
+                        acct_close_rt<PARITY>(a, nar, t0 + x, px, st, tr, cap);
                     a.ps1 += lg ? (uint64_t)qx : (uint64_t)0 - (uint64_t)qx;
                     a.ps2 += (uint64_t)q2x;
                     a.pos = 0;

@@ -232,6 +232,42 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, cons
     acct_close<PARITY, SEG, false>(a, unused, t, px, st, tr, cap);
 }
 
+// Unsplit runs' close with the width of gap / mdd chosen at run time: `narrow` (wave-uniform, a
+// scalar branch, so the caller keeps one copy of its loop) keeps both in the low words of the
+// int64 fields — both are >= 0 and, while the closes' total variation allows (Acct32), < 2^31,
+// so the high words stay 0.
+template <bool PARITY>
+__device__ __forceinline__ void acct_close_rt(TradeAcct& a, bool narrow, int t, int32_t px,
+                                              const Agg& st, bt_trade* tr, int cap) {
+    const bool lg = a.pos > 0;
+    const int32_t lo = lg ? st.mn - a.ce : a.ce - st.mx;
+    const int32_t hi = lg ? st.mx - a.ce : a.ce - st.mn;
+    const int32_t path = lg ? st.dd : st.du;
+    const int32_t pnl = lg ? px - a.ce : a.ce - px;
+    if (narrow) {
+        const int32_t g = (int32_t)a.gap, m = (int32_t)a.mdd;
+        a.mdd = (uint32_t)max(m, max(g - lo, path));
+        a.gap = (uint32_t)(max(g, hi) - pnl);
+    } else {
+        a.mdd = max(a.mdd, max(a.gap - (int64_t)lo, (int64_t)path));
+        a.gap = max(a.gap, (int64_t)hi) - pnl;
+    }
+    a.R += pnl;
+    a.expo += t - a.e;
+    a.h += trade_term(a.e, t, lg);
+    if (PARITY && a.ntr < cap) {
+        bt_trade r;
+        r.entry_bar = a.e;
+        r.exit_bar = t;
+        r.side = a.pos;
+        r.pad = 0;
+        r.entry_px = a.ce;
+        r.exit_px = px;
+        tr[a.ntr] = r;
+    }
+    a.ntr++;
+}
+
 __device__ __forceinline__ void acct_open(TradeAcct& a, int t, int b, int32_t px) {
     a.e = t;
     a.ce = px;
