@@ -114,7 +114,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
     if (kind == 1) {
         L.stl = take((size_t)ns * kLH * 4);  // lows, highs, block and in-block suffix extrema
         L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
-        L.words = take((size_t)2 * (2 * na * nb + 2 * na) * 8);
+        L.words = take((size_t)2 * (na * nb + 2 * na) * 8);
         L.win = take((size_t)na * 4);
         L.lev = take((size_t)2 * 2 * nlev * kTile);  // first-passage bars, [tile & 1][side][level][bar]
         L.levp = take((size_t)3 * 2 * nlev * kTile * 4);  // the levels (int32), [tile % 3][side][level][bar]
@@ -892,7 +892,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int32_t* crow = close + sd.off;
     const int32_t* hrow = high + sd.off;
     const int32_t* lrow = low + sd.off;
-    const int nword = 2 * nw * nk + 2 * nw;
+    // condition words of a tile: per (window, k) the |z| > k word, then per window the D >= 0
+    // and D <= 0 words (the walk forms [z < -k] = |z| > k and not D >= 0, [z > k] likewise)
+    const int nword = nw * nk + 2 * nw;
     const int winreg = lane < nw ? g.a[lane] : 1;  // window lengths, lane = window (no LDS trip)
     const int64_t kd2 = (int64_t)g.k_den * g.k_den;
     const double kd2d = (double)kd2;
@@ -1107,9 +1109,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const double lh = (Dd * Dd) * kd2d;
             const uint64_t vm = ballot(valid);
             const uint64_t dp = ballot(valid && Dd >= 0.0), dn = ballot(valid && Dd <= 0.0);
-            const uint64_t zneg = vm & ~dp, zpos = vm & ~dn;  // D < 0, D > 0
-            // z tests of one k: lane 4 qq .. 4 qq + 3 of `zw` collect its words (v_writelane, lane
-            // = dword of Wd[2 (ow nk + q) + side]), one store per pass of kMaxK values; a
+            // z tests of one k: lanes 2 qq, 2 qq + 1 of `zw` collect its |z| > k word (v_writelane,
+            // lane = dword of Wd[ow nk + q]; the walk splits it by the sign of D), one store per
+            // pass of kMaxK values; a
             // lane the fp64 bracket cannot settle marks the k in `unc` (wave-uniform), and the
             // pass then settles those k exactly in int128, once, outside the unrolled tests
             auto ztest = [&](auto qtag, double kn2, uint32_t& zw, uint32_t& unc) {
@@ -1117,11 +1119,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 const uint64_t big = vcmp_gt_f64(lh, kn2 * QH) & vm;
                 const uint64_t small = vcmp_gt_f64(kn2 * QL, lh);
                 if (vm & ~big & ~small) unc |= 1u << qq;
-                const uint64_t zl = big & zneg, zh = big & zpos;
-                writelane<4 * qq>(zw, (uint32_t)zl);
-                writelane<4 * qq + 1>(zw, (uint32_t)(zl >> 32));
-                writelane<4 * qq + 2>(zw, (uint32_t)zh);
-                writelane<4 * qq + 3>(zw, (uint32_t)(zh >> 32));
+                writelane<2 * qq>(zw, (uint32_t)big);
+                writelane<2 * qq + 1>(zw, (uint32_t)(big >> 32));
             };
             auto settle = [&](int q0, uint32_t unc, uint32_t& zw) {  // rare
                 // the exact integers behind the doubles, re-read from the rings (nothing stays live
@@ -1140,10 +1139,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     unc &= unc - 1;
                     const int64_t kn = g.b[q0 + qq];
                     const uint64_t big = sgpr64(ballot(valid && (i128)Dv * (i128)Dv * (i128)kd2 > (i128)(kn * kn) * (i128)Q));
-                    const uint64_t zl = big & zneg, zh = big & zpos;
-                    const int d = lane - 4 * qq;  // lane 4 qq + d holds dword d of (zl, zh)
-                    if (d >= 0 && d < 4)
-                        zw = (uint32_t)((d < 2 ? zl : zh) >> (32 * (d & 1)));
+                    const int d = lane - 2 * qq;  // lane 2 qq + d holds dword d of big
+                    if (d >= 0 && d < 2) zw = (uint32_t)(big >> (32 * d));
                 }
             };
             {  // first pass: k_num^2 from the kernel arguments
@@ -1153,7 +1150,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     if (qq < nk) ztest(qtag, g.kn2[qq], zw, unc);
                 });
                 if (unc) settle(0, unc, zw);
-                if (lane < 4 * min(nk, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * ow * nk)[lane] = zw;
+                if (lane < 2 * min(nk, kMaxK)) reinterpret_cast<uint32_t*>(Wd + ow * nk)[lane] = zw;
             }
 #pragma unroll 1
             for (int q0 = kMaxK; q0 < nk; q0 += kMaxK) {  // grids of more than 8 k values
@@ -1163,11 +1160,11 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     if (q0 + qq < nk) ztest(qtag, kn2d[q0 + qq], zw, unc);
                 });
                 if (unc) settle(q0, unc, zw);
-                if (lane < 4 * min(nk - q0, kMaxK)) reinterpret_cast<uint32_t*>(Wd + 2 * (ow * nk + q0))[lane] = zw;
+                if (lane < 2 * min(nk - q0, kMaxK)) reinterpret_cast<uint32_t*>(Wd + ow * nk + q0)[lane] = zw;
             }
             if (lane == 0) {
-                Wd[2 * nw * nk + 2 * ow] = dp;
-                Wd[2 * nw * nk + 2 * ow + 1] = dn;
+                Wd[nw * nk + 2 * ow] = dp;
+                Wd[nw * nk + 2 * ow + 1] = dn;
             }
             if (STAMPS) sa.task[0] += __builtin_amdgcn_s_memtime() - tt0;
             o = grab_value(vn) - base;
@@ -1269,12 +1266,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             const int32_t* LO = lhs_ + s * kLH;
             const uint64_t* W = words + (k & 1) * nword;
             const uint64_t vm = bar_range_mask(t0, w - 1, B - 2);
-            const uint64_t ZL = W[2 * (iw * nk + ik)] & vm, ZH = W[2 * (iw * nk + ik) + 1] & vm;
+            const uint64_t Zb = W[iw * nk + ik] & vm;
+            const uint64_t dpw = W[nw * nk + 2 * iw], dnw = W[nw * nk + 2 * iw + 1];
+            const uint64_t ZL = Zb & ~dpw, ZH = Zb & ~dnw;  // z < -k (D < 0), z > k (D > 0)
             // signal exits with the forced exit at bar B-1 folded in (in this tile iff bl < 64)
             const int bl = B - 1 - t0;
             const uint64_t fb = bl < kTile ? (1ULL << bl) : 0ULL;
-            const uint64_t DP = (W[2 * nw * nk + 2 * iw] & vm) | fb;
-            const uint64_t DN = (W[2 * nw * nk + 2 * iw + 1] & vm) | fb;
+            const uint64_t DP = (dpw & vm) | fb;
+            const uint64_t DN = (dnw & vm) | fb;
             const uint8_t* TL = levt + (k & 1) * 2 * nlev * kTile;  // first-passage tables
             const uint8_t* TH = TL + nlev * kTile;
             const int32_t* PL = levp + (k % 3) * 2 * nlev * kTile;  // levels
