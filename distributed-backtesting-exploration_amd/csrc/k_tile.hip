@@ -212,6 +212,34 @@ __device__ __forceinline__ uint64_t vcmp_gt_f64(double a, double b) {
     return m;
 }
 
+// Lane masks of 0 <= a, a <= 0 (fp64) and w <= x (int32, w wave-uniform), likewise straight from
+// the compare (a ballot of a bool that is not itself a compare costs two VALU more: the bool is
+// materialised in a VGPR and compared again).
+__device__ __forceinline__ uint64_t vcmp_ge0_f64(double a) {
+    uint64_t m;
+    asm volatile("v_cmp_le_f64_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+__device__ __forceinline__ uint64_t vcmp_le0_f64(double a) {
+    uint64_t m;
+    asm volatile("v_cmp_ge_f64_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+__device__ __forceinline__ uint64_t vcmp_le_i32(int32_t w, int32_t x) {
+    uint64_t m;
+    asm volatile("v_cmp_le_i32_e64 %0, %1, %2" : "=s"(m) : "s"(w), "v"(x));
+    return m;
+}
+
+// `bit` if the lane mask m is not empty, else 0, in two scalar instructions (the compiler turns
+// the same test into a VGPR bool and a readfirstlane when the result is a zero-extended flag)
+template <uint32_t bit>
+__device__ __forceinline__ uint32_t any_bit(uint64_t m) {
+    uint32_t r;
+    asm volatile("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, %2, 0" : "=s"(r) : "s"(m), "i"(bit) : "scc");
+    return r;
+}
+
 // v_writelane: lane L of v takes the wave-uniform x.
 template <int L>
 __device__ __forceinline__ void writelane(uint32_t& v, uint32_t x) {
@@ -1047,6 +1075,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const double P1t = r1[ptop];
         const double2 P2t = r2[ptop];
         const double cdw = (double)c;
+        const uint64_t tin = ballot(t < B);  // bars of the tile inside the series
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
@@ -1107,8 +1136,8 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             // A valid lane with neither (both sides zero included, or a window so flat that Q is
             // inside the bracket) is settled exactly in int128 with its whole wave.
             const double lh = (Dd * Dd) * kd2d;
-            const uint64_t vm = ballot(valid);
-            const uint64_t dp = ballot(valid && Dd >= 0.0), dn = ballot(valid && Dd <= 0.0);
+            const uint64_t vm = vcmp_le_i32(Wn, t + 1) & tin;  // ballot(valid)
+            const uint64_t dp = vcmp_ge0_f64(Dd) & vm, dn = vcmp_le0_f64(Dd) & vm;
             // z tests of one k: lanes 2 qq, 2 qq + 1 of `zw` collect its |z| > k word (v_writelane,
             // lane = dword of Wd[ow nk + q]; the walk splits it by the sign of D), one store per
             // pass of kMaxK values; a
@@ -1118,7 +1147,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 constexpr int qq = decltype(qtag)::value;
                 const uint64_t big = vcmp_gt_f64(lh, kn2 * QH) & vm;
                 const uint64_t small = vcmp_gt_f64(kn2 * QL, lh);
-                if (vm & ~big & ~small) unc |= 1u << qq;
+                unc |= any_bit<1u << qq>(vm & ~big & ~small);
                 writelane<2 * qq>(zw, (uint32_t)big);
                 writelane<2 * qq + 1>(zw, (uint32_t)(big >> 32));
             };
