@@ -212,7 +212,7 @@ __device__ __forceinline__ uint64_t vcmp_gt_f64(double a, double b) {
     return m;
 }
 
-// Lane masks of 0 <= a, a <= 0 (fp64) and w <= x (int32, w wave-uniform), likewise straight from
+// Lane masks of 0 <= a, a <= 0 (fp64, int64) and w <= x (int32, w wave-uniform), likewise straight from
 // the compare (a ballot of a bool that is not itself a compare costs two VALU more: the bool is
 // materialised in a VGPR and compared again).
 __device__ __forceinline__ uint64_t vcmp_ge0_f64(double a) {
@@ -223,6 +223,16 @@ __device__ __forceinline__ uint64_t vcmp_ge0_f64(double a) {
 __device__ __forceinline__ uint64_t vcmp_le0_f64(double a) {
     uint64_t m;
     asm volatile("v_cmp_ge_f64_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+__device__ __forceinline__ uint64_t vcmp_ge0_i64(int64_t a) {
+    uint64_t m;
+    asm volatile("v_cmp_le_i64_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+__device__ __forceinline__ uint64_t vcmp_le0_i64(int64_t a) {
+    uint64_t m;
+    asm volatile("v_cmp_ge_i64_e64 %0, 0, %1" : "=s"(m) : "v"(a));
     return m;
 }
 __device__ __forceinline__ uint64_t vcmp_le_i32(int32_t w, int32_t x) {
@@ -522,6 +532,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         const double* E = ebuf + (T & 1) * estage;
         const int ptop = ring_pos(T, lane, R);
         const uint64_t P1t = r1[ptop], P2t = r2[ptop];
+        const uint64_t tin = ballot(t < B);  // bars of the tile inside the series
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
 #pragma unroll 1
@@ -530,8 +541,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             const bool hs = (int)o < nsp, ho = (int)o < nol;  // wave-uniform
             const int Wn = nol <= 64 ? __builtin_amdgcn_readlane(winreg, (int)o & 63) : win[o];
             const int pj = ring_back(ptop, Wn, R);
-            const double e = hs ? E[o * kEStride + lane] : 0.0;
-            const uint64_t r1j = ho ? r1[pj] : 0, r2j = ho ? r2[pj] : 0;
+            // unconditional reads at clamped / valid addresses (a task without a span or a window
+            // leaves them unused): no select on the task's kind, which the compiler builds as a
+            // VGPR bool
+            const double e = E[min((int)o, nsp - 1) * kEStride + lane];
+            const uint64_t r1j = r1[pj], r2j = r2[pj];
             if (hs) {  // span: entry / exit conditions against the EMA
                 const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
                 const uint64_t wx = __ballot(cd >= e), wy = __ballot(cd <= e);
@@ -544,11 +558,13 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             }
             if (ho) {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
                 const int jj = t + 1 - Wn;
-                const bool valid = jj >= 0 && t < B;
+                const uint64_t vm = vcmp_le_i32(Wn, t + 1) & tin;  // jj >= 0 && t < B
                 // 2 (sum i c_i - jj S) - (w - 1) S with one multiply
                 const uint64_t S = P1t - r1j;
                 const int64_t N = (int64_t)(2 * (P2t - r2j) - (uint64_t)(int64_t)(2 * jj + Wn - 1) * S);
-                const uint64_t wp = __ballot(valid && N >= 0), wn = __ballot(valid && N <= 0);
+                // (masks straight from the compares: a ballot of `valid && N >= 0` is a VGPR bool
+                // compared again)
+                const uint64_t wp = vcmp_ge0_i64(N) & vm, wn = vcmp_le0_i64(N) & vm;
                 if (lane == 0) {
                     Wd[4 * nsp + 2 * o] = wp;
                     Wd[4 * nsp + 2 * o + 1] = wn;
