@@ -35,6 +35,20 @@ def compare_summary(gpu, orc, where=""):
     assert g == o, f"{where}: sharpe not bit-exact {g!r} vs {o!r}"
 
 
+def compare_summaries(gpu, orc, where):
+    """Bit-exact comparison of two equal-shape summary arrays (every field, Sharpe by bits);
+    the first mismatch is reported through compare_summary with where(index)."""
+    assert gpu.shape == orc.shape, f"shapes {gpu.shape} vs {orc.shape}"
+    bad = np.zeros(gpu.shape, dtype=bool)
+    for f in FIELDS:
+        bad |= gpu[f].astype(np.int64) != orc[f].astype(np.int64)
+    bad |= gpu["sharpe"].astype(np.float64).view(np.uint64) != orc["sharpe"].astype(np.float64).view(np.uint64)
+    if bad.any():
+        i = tuple(int(x) for x in np.argwhere(bad)[0])
+        compare_summary(gpu[i], orc[i], where(i))
+        raise AssertionError(f"{where(i)}: summaries differ")
+
+
 def compare_trades(gpu_tr, orc_tr, n, where=""):
     got = [tuple(int(x) for x in (t["entry_bar"], t["exit_bar"], t["side"], t["entry_px"], t["exit_px"]))
            for t in gpu_tr[:n]]

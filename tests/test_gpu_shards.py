@@ -8,7 +8,7 @@ only parallelism is file-level job farming, /root/reference/src/server/main.rs:1
   merge of the exchange) and the summed counters.
 * Strong-scaling shards (config 4 on 8 GPUs, config 3 on 2 GPUs: 250 x 98,280 each): the
   automatic bar split runs (>= 2 segments), equals the unsplit kernel over all 250 symbols, and
-  every parameter of sampled symbols matches the C oracle."""
+  every parameter of every symbol matches the C oracle."""
 import os
 
 import numpy as np
@@ -17,7 +17,7 @@ import pytest
 import dbx_amd as D
 import orc_ffi as F
 from dbx_amd import parallel as PAR
-from helpers import compare_summary
+from helpers import compare_summaries
 
 pytestmark = pytest.mark.gpu
 
@@ -88,8 +88,7 @@ def test_strong_scaling_shard_full_shape(config, world, rank):
     assert used >= 2
     assert split.tobytes() == unsplit.tobytes(), "split shard differs from the unsplit kernel"
     assert st_split["trades"] == st_unsplit["trades"] == int(split["n_trades"].sum())
-    rng = np.random.default_rng(config)
-    sample = sorted(int(s) for s in rng.choice(n, 8, replace=False))
+    sample = list(range(n))  # every symbol of the shard (the oracle's pool: seconds)
     cols = [F.gen(SEED, sym0 + s, bars, 1) for s in sample]
     closes = np.stack([c[3] for c in cols])
     if config == 3:
@@ -98,6 +97,4 @@ def test_strong_scaling_shard_full_shape(config, world, rank):
         orc = F.boll_grid_mt(np.stack([c[1] for c in cols]), np.stack([c[2] for c in cols]), closes,
                              grid.axes[0], grid.axes[1], grid.k_den, grid.axes[2], grid.axes[3],
                              98280, _threads())
-    for i, s in enumerate(sample):
-        for p in range(grid.n_params):
-            compare_summary(split[s, p], orc[i, p], f"config {config} sym {sym0 + s} {grid.param(p)}")
+    compare_summaries(split, orc, lambda i: f"config {config} sym {sym0 + i[0]} {grid.param(i[1])}")
