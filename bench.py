@@ -250,16 +250,21 @@ def main():
         # and its run counters (summed on the host), in the C-ABI exchange's byte format
         return PAR.exchange(top, topk, [n_sym * BARS * P, trades], dist)
 
+    wait_s = [0.0]  # host time blocked in finish() (the read-back / exchange wait) this run
+
     def steps(n):
         """n steps; step i+1 is enqueued before step i's read-back and exchange, so the GPU runs
         the next pass while the host consumes (and, for N > 1, exchanges) this one."""
         res = (None, None)
+        wait_s[0] = 0.0
         if n > 0:
             issue(0)
         for i in range(n):
             if i + 1 < n:
                 issue(i + 1)
+            tw = time.perf_counter()
             res = finish(i)
+            wait_s[0] += time.perf_counter() - tw
         return res
 
     steps(args.warmup)
@@ -276,12 +281,26 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64,
-                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     kms, launches, kname = eng.kernel_timing()
+    per_rank = None
+    if dist is not None:
+        # max over ranks of the timed region; and, gathered once after it, every rank's own
+        # kernel average (HIP events) and host wait for the read-back / exchange per step, so a
+        # scaling loss can be told apart: load imbalance (kernel times differ) vs the exchange
+        # (kernel times equal, waits grow)
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        mine = torch.tensor([elapsed, kms / max(launches, 1), wait_s[0] * 1e3 / max(args.steps, 1),
+                             float(n_sym)], dtype=torch.float64, device=dev)
+        alls = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(alls, mine)
+        rows = torch.stack(alls).cpu().numpy()
+        elapsed = float(rows[:, 0].max())
+
+        def mm(col):
+            return {"min": float(rows[:, col].min()), "max": float(rows[:, col].max()),
+                    "by_rank": [float(x) for x in rows[:, col]]}
+        per_rank = {"kernel_avg_ms": mm(1), "exchange_wait_ms_per_step": mm(2),
+                    "timed_region_s": mm(0), "symbols": [int(x) for x in rows[:, 3]]}
     stats = eng.stats()
     # bar segments per symbol of the last run and the blocks its fix passes re-walked (read
     # after the timed region: the count is a device read-back)
@@ -342,6 +361,8 @@ def main():
             "top1": {"sharpe": float(top[0]["sharpe"]), "sym": int(top[0]["sym"]),
                      "param": int(top[0]["param"])} if top is not None and len(top) else None,
         }
+        if per_rank is not None:
+            line["per_rank"] = per_rank
         if verified is not None:
             line["verified_exchange"] = verified
         if world == 1 and not args.no_cpu_baseline:

@@ -274,10 +274,15 @@ int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
 
 int64_t bt_exchange_message_bytes(int32_t k) { return k < 1 ? -1 : (int64_t)message_bytes(k); }
 
-int32_t bt_exchange_merge(const uint8_t* block, int32_t world, int32_t k_msg, bt_topk_rec* out,
-                          int32_t k, int64_t* counters) {
+int32_t bt_exchange_merge(const uint8_t* block, size_t block_bytes, int32_t world, int32_t k_msg,
+                          bt_topk_rec* out, int32_t k, int64_t* counters) {
     try {
         if (!block || world < 1 || k_msg < 1 || !out || k < 1) throw CommFail{"bad arguments"};
+        // a short or mismatched block (a truncated gather, a rank that sent another k) is
+        // rejected, never read past its end
+        if (block_bytes != (size_t)world * message_bytes(k_msg))
+            throw CommFail{"block holds " + std::to_string(block_bytes) + " bytes, not world x " +
+                           std::to_string(message_bytes(k_msg))};
         return merge_block(block, world, k_msg, out, k, counters);
     } catch (const CommFail& f) {
         set_last_error(f.msg);

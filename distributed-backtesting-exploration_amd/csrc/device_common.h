@@ -18,9 +18,6 @@ __host__ __device__ inline uint64_t trade_mix(uint64_t w) {
 // (w >> 29 has lo = t << 2 and hi = side << 1 in that range; checked against trade_mix on 5e7
 // random terms, and bit for bit by every GPU parity test through the hash).
 __host__ __device__ inline uint64_t trade_mix_et(uint32_t e, uint32_t t, bool lg) {
-#if defined(BT_HASH_PLAIN)  // A/B aid: the generic form
-    return trade_mix((uint64_t)e | ((uint64_t)t << 31) | ((uint64_t)lg << 62));
-#endif
     const uint32_t lo = e ^ (t << 2) ^ (t << 31);
     const uint32_t hi = (t >> 1) ^ (lg ? 0x40000002u : 0u);
     const uint64_t z = (((uint64_t)hi << 32) | lo) * 0xBF58476D1CE4E5B9ULL;

@@ -38,26 +38,13 @@ constexpr int kKS = kTile + 4;        // int32 key row stride: rows 16-B aligned
 constexpr int kStages = 3;            // tile buffers in flight (cT, Q)
 constexpr int kDstStages = 2;         // drawdown tables: built in interval k - 1, read in k
 constexpr int kKeyGrab = 4;           // windows per key task (one LDS atomic per group)
-#ifndef BT_CMP_DEPTH1
-#define BT_CMP_DEPTH1 2
-#endif
-constexpr int kCmpDepth1 = BT_CMP_DEPTH1;  // key-row pairs in flight in a ONE_TRIP compare
-// Stage 1 as a task of the stage-2 round (any wave) instead of a fixed duty of the last wave,
-// for blocks whose last wave also walks parameters (BT_S1TASK_16, config 5's 16-wave blocks) or
-// for every block (BT_S1TASK_ALL). Measured (round 4, interleaved A/B): config 5's shard
-// 137.6 -> 137.6-137.9 ms (neutral), config 2 1.16 -> 1.21 ms; both off by default.
-#ifndef BT_S1TASK_16
-#define BT_S1TASK_16 0
-#endif
-#ifndef BT_S1TASK_ALL
-#define BT_S1TASK_ALL 0
-#endif
 // Key-row pairs in flight in the 16-wave (ONE_TRIP) compare: 2, 4, 8 and 16 are within 0.5 %
 // of each other on config 5's shard (round 4); the whole 10,000-symbol workload ran 3 % slower
 // with 16 and no VGPR cap, so 2.
+constexpr int kCmpDepth1 = 2;
 
 struct SmaLds {                       // byte offsets into dynamic LDS
-    size_t ring, keys, invw, win, dst, ct, ql, nar, stc, cyl, ctr, total;
+    size_t ring, keys, invw, win, dst, ct, ql, nar, ctr, total;
 };
 
 __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
@@ -73,8 +60,6 @@ __host__ __device__ inline SmaLds sma_lds_layout(int ring, int nw) {
     L.ct = take((size_t)kStages * kTile * 4);
     L.ql = take((size_t)kStages * 2 * kTile * 8);
     L.nar = take((size_t)kStages * 4);    // per tile stage: accounts fit int32 (SmaAcct)
-    L.stc = take((size_t)2 * kTile * 4);  // stage-1 task: the closes of its tile, [tile & 1]
-    L.cyl = take(16);                     // stage-1 task: the scan carry (ScanCarry)
     L.ctr = take(4);
     L.total = o;
     return L;
@@ -154,60 +139,36 @@ __device__ __forceinline__ int32_t floor_key(double F, double iw) {
     return (int32_t)(F * iw);
 }
 
-// Counter values of one stage-2 round: the stage-1 task (s1 = 1), the drawdown-table task, the
-// key groups, and one failing grab per wave.
-__host__ __device__ inline uint32_t key_round_len(int nwp, int nwaves, int s1) {
-    return (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + 1 + (uint32_t)s1 + (uint32_t)nwaves);
+// Counter values of one stage-2 round: the drawdown-table task, the key groups, and one failing
+// grab per wave.
+__host__ __device__ inline uint32_t key_round_len(int nwp, int nwaves) {
+    return (uint32_t)kKeyGrab * ((uint32_t)nwp / kKeyGrab + 1 + (uint32_t)nwaves);
 }
-
-// The stage-1 task of a round: tile T's closes from the LDS slot the last wave staged them in
-// (stc, one interval earlier), the scan carry from LDS, stage_ring, the carry back.
-struct Stage1Task {
-    int T;                  // tile to scan this round (-1: none)
-    const int32_t* stc;     // staged closes [T & 1][64]
-    ScanCarry* cyl;         // the carry between tiles
-    int32_t* cts;
-    int64_t* qls;
-    int32_t* nars;
-};
 
 // Stage 2 of round r (tile r): the tile's drawdown table (device_common.h dst_build) from the
 // closes stage 1 left in LDS (cTr), into Dr, as the round's first task, then the key groups.
 // The table is a task rather than a fixed role: on the half-empty seventh parameter wave of a
 // config-2 block it set the tile (that wave's compare and walk plus the table's DPP chain).
-template <bool S1>
 __device__ __forceinline__ void stage_keys(int t0, int B, int nw, int nwp, int nf, int wmax, int R,
                                            double* ring, const int32_t* win,
                                            const double* invw, int32_t* K, uint32_t* ctr,
                                            uint32_t round, int nwaves, int lane,
-                                           const int32_t* cTr, Agg* Dr, const Stage1Task& s1) {
+                                           const int32_t* cTr, Agg* Dr) {
     const int t = t0 + lane;
     const double top = ring[(t + 1) & (R - 1)];
     // wave-uniform: every bar of the tile has a full window for every window length
     const bool full = t0 + 1 - wmax >= 0 && t0 + kTile <= B;
-    const uint32_t base = round * key_round_len(nwp, nwaves, S1 ? 1 : 0);
+    const uint32_t base = round * key_round_len(nwp, nwaves);
     uint32_t w = __builtin_amdgcn_readlane(grab_issue(ctr, lane), 0) - base;
-    constexpr uint32_t kFirst = S1 ? kKeyGrab : 0;  // counter value of the table task
 #pragma unroll 1
-    while (w < (uint32_t)(nwp + kKeyGrab) + kFirst) {
+    while (w < (uint32_t)(nwp + kKeyGrab)) {
         const uint32_t vn = grab_issue(ctr, lane);  // next group, read at the end
-        if (S1 && w == 0) {  // stage 1 of tile s1.T (a stage-1 dependency chain: grabbed first)
-            if (s1.T >= 0) {
-                const int s = s1.T % kStages;
-                ScanCarry cy = *s1.cyl;
-                stage_ring(s1.stc[(s1.T & 1) * kTile + lane], B, s1.T * kTile, lane, R, ring,
-                           s1.cts + s * kTile, s1.qls + s * 2 * kTile, s1.nars + s, cy);
-                if (lane == 0) *s1.cyl = cy;
-            }
-            w = __builtin_amdgcn_readlane(vn, 0) - base;
-            continue;
-        }
-        if (w == kFirst) {
+        if (w == 0) {  // the table task (counter value 0 of the round)
             dst_build<true>(cTr[lane], lane, Dr);
             w = __builtin_amdgcn_readlane(vn, 0) - base;
             continue;
         }
-        w -= kFirst + kKeyGrab;
+        w -= kKeyGrab;
         // w is a multiple of kKeyGrab: the group's lengths and reciprocals are aligned 16-B
         // reads; rows nw..nwp-1 are padding (length 1) whose keys nobody reads
         int Wv[kKeyGrab];
@@ -441,9 +402,7 @@ __device__ __forceinline__ void sma_flips(SmaAcct& a, uint64_t F, int t0, int bl
 // strict crossover comparison, so one decided bar sets it), and carries the trade open at its
 // first bar symbolically (SmaAcct::carried). The fix pass re-walks a segment whose lanes started
 // in a position other than the previous segment's last one (a burn-in of tied comparisons only).
-// S1: stage 1 is a task of the stage-2 round (Stage1Task): the last wave only stages the closes
-// of the tile after next in LDS and keeps the next load in flight.
-template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool SEG, bool S1>
+template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool SEG>
 __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
                                          const int32_t* __restrict__ close, const Grid& g,
                                          const Out& out, int dedicated, const SegArgs& sg,
@@ -460,8 +419,6 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
     int64_t* qls = reinterpret_cast<int64_t*>(smem + LL.ql);
     int32_t* nars = reinterpret_cast<int32_t*>(smem + LL.nar);
-    int32_t* stc = reinterpret_cast<int32_t*>(smem + LL.stc);
-    ScanCarry* cyl = reinterpret_cast<ScanCarry*>(smem + LL.cyl);
     uint32_t* ctr = reinterpret_cast<uint32_t*>(smem + LL.ctr);
 
     const int tid = threadIdx.x;
@@ -507,7 +464,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
 
     const int nwp = (nw + kKeyGrab - 1) / kKeyGrab * kKeyGrab;
-    const uint32_t key_round = key_round_len(nwp, nwaves, S1 ? 1 : 0);
+    const uint32_t key_round = key_round_len(nwp, nwaves);
     for (int w = tid; w < nwp; w += blockDim.x) {
         const int W = w < nf ? g.a[w] : (w < nw ? g.b[w - nf] : 1);
         win[w] = W;
@@ -548,9 +505,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         }
     }
     // prologue: stage 1 for the first two walked tiles; stage 2 for the first. The helper keeps
-    // the closes of the tile after next in flight (cpre) across the barrier. S1: it stages that
-    // tile's closes and the carry in LDS for the first round's stage-1 task instead, and keeps the
-    // tile after it in flight.
+    // the closes of the tile after next in flight (cpre) across the barrier.
     int32_t cpre = 0;
     if (helper) {
         const int b0 = T_walk * kTile;
@@ -561,20 +516,13 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         __syncthreads();
         if (T_walk + 1 < T_end)
             stage_ring(c1, B, b0 + kTile, lane, R, ring, cts + s1 * kTile, qls + s1 * 2 * kTile, nars + s1, cy);
-        if (S1) {
-            stc[((T_walk + 2) & 1) * kTile + lane] = cpre;
-            cpre = load_close(crow, B, b0 + 3 * kTile + lane);
-            if (lane == 0) *cyl = cy;
-        }
     } else {
         __syncthreads();
     }
-    const Stage1Task s1none{-1, stc, cyl, cts, qls, nars};
     if (T_walk < T_end)
-        stage_keys<S1>(T_walk * kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw,
-                       keys + (T_walk & 1) * nwp * kKS, ctr, (uint32_t)T_walk, nwaves, lane,
-                       cts + (T_walk % kStages) * kTile, dst + (T_walk % kDstStages) * kDstLevels * kTile,
-                       s1none);
+        stage_keys(T_walk * kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw,
+                   keys + (T_walk & 1) * nwp * kKS, ctr, (uint32_t)T_walk, nwaves, lane,
+                   cts + (T_walk % kStages) * kTile, dst + (T_walk % kDstStages) * kDstLevels * kTile);
     __syncthreads();
 
     SmaAcct a;
@@ -646,14 +594,7 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
         const int t0 = k * kTile;
         // ---- stage 1 (helper, tile k+2), then stage 3 (parameter waves, tile k), then stage 2
         // (tile k+1) on every wave, balanced dynamically
-        if (S1) {
-            // stage the closes of tile k + 3 for the next round's stage-1 task (its slot's last
-            // reader, round k's task, finished before the barrier) and load tile k + 4
-            if (helper && k + 3 < T_end) {
-                stc[((k + 3) & 1) * kTile + lane] = cpre;
-                cpre = load_close(crow, B, t0 + 4 * kTile + lane);
-            }
-        } else if (helper && k + 2 < T_end && !BT_ABL(g, 1)) {
+        if (helper && k + 2 < T_end && !BT_ABL(g, 1)) {
             // stage 1 is a dependent DPP/fp64 chain on one wave: issue it first
             if (!BT_ABL(g, 32)) __builtin_amdgcn_s_setprio(2);
             const int s = (k + 2) % kStages;
@@ -783,10 +724,9 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
             if (ONE_TRIP) __builtin_amdgcn_s_setprio(0);
         }
         if (k + 1 < T_end && !BT_ABL(g, 2))
-            stage_keys<S1>(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
-                           ctr, (uint32_t)(k + 1), nwaves, lane, cts + ((k + 1) % kStages) * kTile,
-                           dst + ((k + 1) % kDstStages) * kDstLevels * kTile,
-                           Stage1Task{k + 2 < T_end ? k + 2 : -1, stc, cyl, cts, qls, nars});
+            stage_keys(t0 + kTile, B, nw, nwp, nf, g.wmax, R, ring, win, invw, keys + ((k + 1) & 1) * nwp * kKS,
+                       ctr, (uint32_t)(k + 1), nwaves, lane, cts + ((k + 1) % kStages) * kTile,
+                       dst + ((k + 1) % kDstStages) * kDstLevels * kTile);
         BT_STAMP(1)
         __syncthreads();
         BT_STAMP(6)
@@ -869,20 +809,20 @@ __device__ __forceinline__ void sma_body(const SymDesc* __restrict__ syms,
     wave_add_trades(out, active ? a.ntr : 0);
 }
 
-template <bool PARITY, bool STAMPS, bool ONE_TRIP, bool S1>
+template <bool PARITY, bool STAMPS, bool ONE_TRIP>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void sma_kernel(
     const SymDesc* __restrict__ syms, const int32_t* __restrict__ close, Grid g, Out out,
     int dedicated) {
-    sma_body<PARITY, STAMPS, ONE_TRIP, false, S1>(syms, close, g, out, dedicated, SegArgs{}, 0);
+    sma_body<PARITY, STAMPS, ONE_TRIP, false>(syms, close, g, out, dedicated, SegArgs{}, 0);
 }
 
 // Bar segments (SMA_SEG): its own kernel, for one-block-per-CU shapes (up to 128 VGPRs).
-template <bool ONE_TRIP, bool S1>
+template <bool ONE_TRIP>
 __global__ __launch_bounds__(1024) void sma_seg_kernel(const SymDesc* __restrict__ syms,
                                                        const int32_t* __restrict__ close, Grid g,
                                                        Out out, int dedicated, SegArgs sg,
                                                        int fix_seg) {
-    sma_body<false, false, ONE_TRIP, true, S1>(syms, close, g, out, dedicated, sg, fix_seg);
+    sma_body<false, false, ONE_TRIP, true>(syms, close, g, out, dedicated, sg, fix_seg);
 }
 
 // Folds the segments of every (symbol, param) in order (internal.h SmaSegRec): the trade open
@@ -1018,7 +958,7 @@ int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
 
 namespace {
 
-template <bool ONE_TRIP, bool S1>
+template <bool ONE_TRIP>
 hipError_t launch_sma_variant(const SymDesc* syms, int32_t n_sym, const int32_t* close,
                               const Grid& g, const Out& out, bool parity, const SegArgs& seg,
                               hipStream_t st, const SmaShape& sh, size_t lds) {
@@ -1028,16 +968,16 @@ hipError_t launch_sma_variant(const SymDesc* syms, int32_t n_sym, const int32_t*
         // when every lane started in the true position), then the fold
         const dim3 sgrid(n_sym, sh.gy, seg.G), fgrid(n_sym, sh.gy, 1);
         for (int s = 0; s < seg.G; ++s)
-            hipLaunchKernelGGL((sma_seg_kernel<ONE_TRIP, S1>), s == 0 ? sgrid : fgrid, block, lds, st, syms,
+            hipLaunchKernelGGL((sma_seg_kernel<ONE_TRIP>), s == 0 ? sgrid : fgrid, block, lds, st, syms,
                                close, g, out, sh.dedicated, seg, s);
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(sma_seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym,
                            g.n_params, reinterpret_cast<const SmaSegRec*>(seg.rec), seg.G, g.sqrt_ann, out);
     } else if (parity) {
-        hipLaunchKernelGGL((sma_kernel<true, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
+        hipLaunchKernelGGL((sma_kernel<true, false, ONE_TRIP>), grid, block, lds, st, syms, close, g, out,
                            sh.dedicated);
     } else {
-        hipLaunchKernelGGL((sma_kernel<false, false, ONE_TRIP, S1>), grid, block, lds, st, syms, close, g, out,
+        hipLaunchKernelGGL((sma_kernel<false, false, ONE_TRIP>), grid, block, lds, st, syms, close, g, out,
                            sh.dedicated);
     }
     return hipGetLastError();
@@ -1058,21 +998,13 @@ hipError_t launch_sma(const SymDesc* syms, int32_t n_sym, const int32_t* close, 
     if (const char* v = getenv("BT_ONE_TRIP")) one_trip = atoi(v) != 0;  // tuning aid
     if (BT_ABL(g, 64)) {
         const dim3 grid(n_sym, sh.gy), block(sh.block);
-        if (sh.dedicated)
-            hipLaunchKernelGGL((sma_kernel<false, true, false, BT_S1TASK_ALL != 0>), grid, block, lds, st,
-                               syms, close, g, out, sh.dedicated);
-        else
-            hipLaunchKernelGGL((sma_kernel<false, true, false, BT_S1TASK_16 != 0>), grid, block, lds, st,
-                               syms, close, g, out, sh.dedicated);
+        hipLaunchKernelGGL((sma_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out,
+                           sh.dedicated);
         return hipGetLastError();
     }
 #endif
-    // stage 1 as a stage-2 task when the last wave also walks parameters (no dedicated helper)
-    const bool s1 = (!sh.dedicated && BT_S1TASK_16) || BT_S1TASK_ALL;
-    if (one_trip && s1) return launch_sma_variant<true, true>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
-    if (one_trip) return launch_sma_variant<true, false>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
-    if (s1) return launch_sma_variant<false, true>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
-    return launch_sma_variant<false, false>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
+    if (one_trip) return launch_sma_variant<true>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
+    return launch_sma_variant<false>(syms, n_sym, close, g, out, parity, seg, st, sh, lds);
 }
 
 }  // namespace bt

@@ -58,27 +58,12 @@ constexpr int kBollStages = 4;
 // Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
 // after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
 constexpr int kRecCap = 33;
-#ifndef BT_CHAIN_OPAQUE
-#define BT_CHAIN_OPAQUE 0
-#endif
-#ifndef BT_CHAIN_SB
-#define BT_CHAIN_SB 0
-#endif
 
 // EMA+OLS walk accounts in int32 while the closes' total variation allows (unsplit runs)
 #ifndef BT_EMA_NARROW
 #define BT_EMA_NARROW 1
 #endif
 constexpr bool kEmaNarrow = BT_EMA_NARROW;
-#ifndef BT_EMA_NAR_LDS
-#define BT_EMA_NAR_LDS 1
-#endif
-
-// bar segments' accountant in int32 while the segment's total variation allows (Acct32 SEG forms)
-#ifndef BT_BOLL_SEG_NARROW
-#define BT_BOLL_SEG_NARROW 0
-#endif
-constexpr bool kBollSegNarrow = BT_BOLL_SEG_NARROW;
 
 // the Bollinger walkers' (unsplit parameter waves') gap / mdd in int32 while the closes' total
 // variation allows (unsplit runs; tile_common.h acct_close_rt)
@@ -128,9 +113,7 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.ebuf = take((size_t)2 * na * kEStride * 8);
         L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
         L.win = take((size_t)nb * 4);
-#if BT_EMA_NAR_LDS
         L.nar = take((size_t)ns * 4);  // per tile stage: the walk's accounts fit int32 (Acct32)
-#endif
     }
     L.ctr = take(4);
     L.total = o;
@@ -466,19 +449,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 for (int b = 0; b < kTile; ++b) E[b] = (double)__builtin_amdgcn_readlane(cl, b);
             } else if ((chain_b0 < t1 || chain_b0 >= t1 + kTile) && t1 + kTile <= B) {
                 // 8 bars' closes read one chunk ahead (the reads precede, in program order, the
-                // chain's stores that may alias them). BT_CHAIN_OPAQUE addresses both rows from
-                // opaque LDS pointers (immediate offsets, no v_add / v_mov per ds_write2 /
-                // ds_read2): measured 6 % slower on config 3 (the compiler then cannot tell the
-                // rows apart and schedules the reads behind the stores), so off
-#if BT_CHAIN_OPAQUE
-                lds_f64* Ev = (lds_f64*)E;
-                const lds_f64* Cv = (const lds_f64*)CD;
-                asm volatile("" : "+v"(Ev));
-                asm volatile("" : "+v"(Cv));
-#else
+                // chain's stores that may alias them; opaque LDS pointers with immediate offsets
+                // measured 6 % slower: DESIGN.md Appendix A)
                 double* Ev = E;
                 const double* Cv = CD;
-#endif
                 double nx[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) nx[u] = Cv[u];
@@ -495,9 +469,6 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     for (int u = 0; u < 8; ++u) {
                         ema = ema + alpha * (cur[u] - ema);
                         Ev[8 * c + u] = ema;
-#if BT_CHAIN_SB
-                        if (u & 1) __builtin_amdgcn_sched_barrier(0);  // store each pair at once
-#endif
                     }
                 }
             } else {
@@ -658,7 +629,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 // loop per width, chosen per tile (wave-uniform)
                 auto trades = [&](auto narrow_tag) {
                     constexpr bool NARROW = decltype(narrow_tag)::value;
-                    Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd, 0, 0, 0};  // <= TV < 2^30 if NARROW
+                    Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd};  // <= TV < 2^30 if NARROW
                     uint64_t Ev = Ev0, Xv = Xv0;
                     if (a.pos != 0 && Xv) {  // the position carried in closes first
                         const int x = __builtin_ctzll(Xv);
@@ -1493,12 +1464,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             auto records = [&](auto narrow_tag) {
                 constexpr bool NARROW = decltype(narrow_tag)::value;
                 // gap, mdd (SEG: the forms) within 2 TV < 2^31 if NARROW
-                Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd, 0, 0, 0};
-                if (SEG && NARROW) {
-                    n32.B = form_to32(a.Bq);
-                    n32.C = form_to32(a.C);
-                    n32.D = form_to32(a.D);
-                }
+                Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd};
 #pragma unroll 1
                 for (int i = 0; i < n; ++i) {
                     if (STAMPS) sa.count(3);
@@ -1530,17 +1496,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         close_trade(narrow_tag, n32, ta, x, qi, px, seg, qx, q2x);
                     }
                 }
-                if (NARROW && SEG) {
-                    a.Bq = form_to64(n32.B);
-                    a.C = form_to64(n32.C);
-                    a.D = form_to64(n32.D);
-                } else if (NARROW) {
+                if (NARROW) {
                     a.gap = (uint32_t)n32.g;  // >= 0
                     a.mdd = (uint32_t)n32.m;
                 }
             };
-            // the fix pass writes no flags (its injected trade may predate the segment's scan)
-            if ((!SEG || (kBollSegNarrow && fix_seg == 0)) && __builtin_amdgcn_readfirstlane(nars[s]))
+            // unsplit runs only (bar segments keep the wide max-plus forms)
+            if (!SEG && __builtin_amdgcn_readfirstlane(nars[s]))
                 records(std::true_type{});
             else
                 records(std::false_type{});
@@ -1666,20 +1628,6 @@ static bool tile_split_walk() {
     return on;
 }
 
-// Second finder/accountant pair (the second-busiest z threshold): off unless built with
-// -DBT_SPLIT2 (A/B build) or, in the profiling build, BT_SPLIT2=1.
-static bool tile_split_walk2() {
-#ifdef BT_SPLIT2
-    bool on = true;
-#else
-    bool on = false;
-#endif
-#ifdef BT_PROFILING
-    if (const char* v = getenv("BT_SPLIT2")) on = atoi(v) != 0;
-#endif
-    return on;
-}
-
 static int tile_lanes_per_wave() {
     int l = 64;
 #ifdef BT_PROFILING
@@ -1794,17 +1742,6 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
         const long long per_k = (long long)g.na * g.nc * g.nd;  // lanes per z threshold
         const int grp = (int)((g.kmin_idx * per_k) / lpw);
         if (grp < pw) split_grp = grp;
-        // the second-smallest threshold trades next most (config 4: 4.3 walk iterations per
-        // tile against 7.1 for the smallest, 1.0-1.3 for the others): its own finder/accountant
-        // pair, when its group is another wave and the records of both pairs leave two blocks'
-        // LDS on a CU (k values beyond the first 8 are not ranked: kn2 holds 8)
-        int k2 = -1;
-        for (int q = 0; q < std::min(g.nb, 8); ++q)
-            if (q != g.kmin_idx && (k2 < 0 || g.kn2[q] < g.kn2[k2])) k2 = q;
-        const int grp2 = k2 >= 0 ? (int)((k2 * per_k) / lpw) : -1;
-        if (split_grp >= 0 && tile_split_walk2() && pw >= 4 && grp2 >= 0 && grp2 < pw &&
-            grp2 != split_grp && boll_lds_bytes(g, 2) <= 80 * 1024)
-            split_grp2 = grp2;
     }
     const int nsplit = split_grp < 0 ? 0 : (split_grp2 < 0 ? 1 : 2);
     const int base = pw + 1 + nsplit;

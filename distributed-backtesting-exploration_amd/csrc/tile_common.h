@@ -112,29 +112,13 @@ struct I96 {
     __device__ __forceinline__ int64_t hi64() const { return (int64_t)hi; }
     __device__ __forceinline__ uint64_t lo64() const { return lo; }
 };
-// The same interface over a full int128 (A/B aid for the tile kernels: BT_ACC_I128)
-struct I128Acc {
-    i128 v;
-    __device__ __forceinline__ void clear() { v = 0; }
-    __device__ __forceinline__ uint64_t lo64() const { return (uint64_t)v; }
-    __device__ __forceinline__ void add(int64_t x) { v += (i128)x; }
-    __device__ __forceinline__ int64_t hi64() const { return (int64_t)(v >> 64); }
-};
-#ifndef BT_ACC_I128
-#define BT_ACC_I128 0
-#endif
-
 
 struct TradeAcct {
     int32_t pos, e, ce, sb, ntr, expo;  // sb: in-tile bar where the open trade's path resumes
     int64_t R, gap, mdd;
     int64_t Bq, C, D;                   // SEG walks only (A = -R)
     uint64_t ps1, ps2, h;
-#if BT_ACC_I128
-    I128Acc s1, s2;
-#else
     I96 s1, s2;
-#endif
     Agg agg;  // closes [e, tile start - 1] of the open trade (kAggId when e is in this tile)
 };
 
@@ -152,34 +136,19 @@ __device__ __forceinline__ void acct_init(TradeAcct& a) {
 // Close the open trade (a.pos, a.e, a.ce) at global bar t for price px, given the trade's
 // adverse / favourable excursions lo / hi and internal drawdown `path` (all relative to the
 // entry close, in the trade's direction), its pnl and its hash term mix(w).
-// Narrow accounts: while the closes' total variation TV (through the tile's last bar) is below
-// 2^30, gap and mdd — differences of equity or price values, |.| <= TV, and the recursion's
-// intermediates <= 2 TV — are exact in int32 (k_sma.hip SmaAcct has the argument).
-// Bar segments (SEG) keep the max-plus forms A, B, C, D narrow on the same bound, over the
-// segment's own bars (its scan restarts the total variation; the fix pass, whose injected open
-// trade may predate the scan, stays wide): A = -R in [-TV, TV]; B, D either "minus infinity" or in
-// [0, 2 TV] (a trade's path holds its entry, so lo <= 0 <= hi and hi >= pnl); C either minus
-// infinity or in [-TV, 2 TV]. Minus infinity is kNeg32 = INT32_MIN, and kNeg32 - lo = INT32_MIN
-// + |lo| stays below every real value without wrapping.
+// Narrow accounts (unsplit runs): while the closes' total variation TV (through the tile's last
+// bar) is below 2^30, gap and mdd — differences of equity or price values, |.| <= TV, and the
+// recursion's intermediates <= 2 TV — are exact in int32 (k_sma.hip SmaAcct has the argument).
+// Bar segments (SEG) keep the wide max-plus forms.
 struct Acct32 {
     int32_t g, m;        // gap, mdd
-    int32_t B, C, D;     // SEG: the drawdown forms (A = -R)
 };
-constexpr int32_t kNeg32 = INT32_MIN;
-
-__device__ __forceinline__ int32_t form_to32(int64_t x) { return x == kNegInf ? kNeg32 : (int32_t)x; }
-__device__ __forceinline__ int64_t form_to64(int32_t x) { return x == kNeg32 ? kNegInf : (int64_t)x; }
 
 template <bool PARITY, bool SEG = false, bool NARROW = false>
 __device__ __forceinline__ void acct_fold(TradeAcct& a, Acct32& n, int t, int32_t px, int32_t lo,
                                           int32_t hi, int32_t path, int32_t pnl, uint64_t mix,
                                           bt_trade* tr, int cap) {
-    if (NARROW && SEG) {
-        const int32_t A0 = -(int32_t)a.R, B0 = n.B;  // A = -R (see TradeAcct)
-        n.C = max(n.C, A0 - lo);
-        n.D = max(n.D, max(B0 - lo, path));
-        n.B = max(B0, hi) - pnl;
-    } else if (NARROW) {
+    if (NARROW && !SEG) {  // (a SEG instantiation of a narrow path is never taken)
         n.m = max(n.m, max(n.g - lo, path));
         n.g = max(n.g, hi) - pnl;
     } else if (SEG) {
@@ -228,7 +197,7 @@ __device__ __forceinline__ void acct_close(TradeAcct& a, Acct32& n, int t, int32
 template <bool PARITY, bool SEG = false>
 __device__ __forceinline__ void acct_close(TradeAcct& a, int t, int32_t px, const Agg& st,
                                            bt_trade* tr, int cap) {
-    Acct32 unused{0, 0, 0, 0, 0};
+    Acct32 unused{0, 0};
     acct_close<PARITY, SEG, false>(a, unused, t, px, st, tr, cap);
 }
 

@@ -229,8 +229,11 @@ class Dispatcher:
                 # oversize_drop_after times while no connected worker's limit admits it
                 rest = files[i:]
                 if not jobs and need > cap:
-                    self.oversize_skips += 1
-                    n = self._oversize_by_path[path] = self._oversize_by_path.get(path, 0) + 1
+                    # request_jobs runs on the server's thread pool: both counters under the
+                    # files lock, so no count is lost and the drop fires exactly once
+                    with self.files_lock:
+                        self.oversize_skips += 1
+                        n = self._oversize_by_path[path] = self._oversize_by_path.get(path, 0) + 1
                     if n >= self.oversize_drop_after and self._no_peer_can_take(need):
                         log.error("%s (%d bytes) exceeds every connected worker's receive limit "
                                   "after %d requests: dropped", path, len(data), n)

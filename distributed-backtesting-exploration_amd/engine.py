@@ -150,21 +150,39 @@ def lib():
     L.bt_encode_columns.restype = C.c_int64
     L.bt_gen_payload.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, P, C.c_size_t]
     L.bt_gen_payload.restype = C.c_int64
-    L.bt_comm_unique_id.argtypes = [P]
-    L.bt_comm_create.argtypes = [P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_size_t]
-    L.bt_comm_create.restype = P
-    L.bt_comm_destroy.argtypes = [P]
-    L.bt_comm_destroy.restype = None
-    L.bt_exchange_async.argtypes = [P, P, C.c_int32]
-    L.bt_exchange_wait.argtypes = [P, C.c_int32, P, C.c_int32, P]
-    L.bt_exchange_message_bytes.argtypes = [C.c_int32]
-    L.bt_exchange_message_bytes.restype = C.c_int64
-    L.bt_exchange_merge.argtypes = [P, C.c_int32, C.c_int32, P, C.c_int32, P]
     L.bt_last_batch_profile.argtypes = [P, C.POINTER(_BatchProfile)]
     L.bt_format_summaries.argtypes = [P, C.c_int32, P, C.c_size_t]
     L.bt_format_summaries.restype = C.c_int64
     _lib = L
     return L
+
+
+# Entry points added after ABI version 2 (the multi-GPU exchange), bound on first use: an older
+# library (e.g. a previous round's build, loaded with BT_LIB for a regression check) then still
+# loads and runs everything else.
+_LATE_SYMBOLS = {
+    "bt_comm_unique_id": ([C.c_void_p], C.c_int32),
+    "bt_comm_create": ([C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_size_t],
+                       C.c_void_p),
+    "bt_comm_destroy": ([C.c_void_p], None),
+    "bt_exchange_async": ([C.c_void_p, C.c_void_p, C.c_int32], C.c_int32),
+    "bt_exchange_wait": ([C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p], C.c_int32),
+    "bt_exchange_message_bytes": ([C.c_int32], C.c_int64),
+    "bt_exchange_merge": ([C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                           C.c_void_p], C.c_int32),
+}
+_late = {}
+
+
+def sym(name: str):
+    """A late (post-v2) entry point of libbt.so, typed on first use; AttributeError if the loaded
+    library predates it."""
+    f = _late.get(name)
+    if f is None:
+        f = getattr(lib(), name)
+        f.argtypes, f.restype = _LATE_SYMBOLS[name]
+        _late[name] = f
+    return f
 
 
 def _check(rc):
@@ -425,7 +443,7 @@ class Comm:
     @staticmethod
     def unique_id() -> bytes:
         buf = C.create_string_buffer(Comm.ID_BYTES)
-        _check(lib().bt_comm_unique_id(buf))
+        _check(sym("bt_comm_unique_id")(buf))
         return buf.raw
 
     def __init__(self, uid: bytes, rank: int, world: int, device: int, k: int):
@@ -433,25 +451,25 @@ class Comm:
             raise ValueError("RCCL unique id must be 128 bytes")
         err = C.create_string_buffer(512)
         self._uid = C.create_string_buffer(bytes(uid), Comm.ID_BYTES)
-        h = lib().bt_comm_create(self._uid, rank, world, device, k, err, 512)
+        h = sym("bt_comm_create")(self._uid, rank, world, device, k, err, 512)
         if not h:
             raise BtError(err.value.decode())
         self._h, self.k, self.world = h, k, world
 
     def exchange_async(self, engine: "Engine", slot: int) -> None:
-        _check(lib().bt_exchange_async(self._h, engine._h, slot))
+        _check(sym("bt_exchange_async")(self._h, engine._h, slot))
 
     def exchange_wait(self, slot: int, k=None) -> tuple:
         """Merged global top-k and [bar-evals, trades] summed over ranks."""
         k = k or self.k
         out = np.zeros(k, TOPK_DTYPE)
         cnt = np.zeros(2, np.int64)
-        m = _check(lib().bt_exchange_wait(self._h, slot, out.ctypes.data, k, cnt.ctypes.data))
+        m = _check(sym("bt_exchange_wait")(self._h, slot, out.ctypes.data, k, cnt.ctypes.data))
         return out[:m], [int(cnt[0]), int(cnt[1])]
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().bt_comm_destroy(self._h)
+            sym("bt_comm_destroy")(self._h)
             self._h = None
 
     __del__ = close
@@ -470,7 +488,7 @@ def exchange_message(records: np.ndarray, k_msg: int, bar_evals: int, trades: in
     """One rank's exchange message as bt_exchange_async sends it (comm.cpp): a header record whose
     first int32 is the record count, k_msg record slots (the first n used), bar-evals, trades."""
     n = len(records)
-    size = _check(lib().bt_exchange_message_bytes(k_msg))
+    size = _check(sym("bt_exchange_message_bytes")(k_msg))
     buf = np.zeros(size, np.uint8)
     buf[:4] = np.frombuffer(np.int32(n).tobytes(), np.uint8)
     rec = TOPK_DTYPE.itemsize
@@ -484,10 +502,14 @@ def exchange_merge(block: bytes, world: int, k_msg: int, k: int) -> tuple:
     """The host half of Comm.exchange_wait (bt_exchange_merge) on a gathered block of `world`
     messages: the merged top-k and [bar-evals, trades] summed over ranks."""
     raw = np.frombuffer(block, np.uint8)
+    need = world * _check(sym("bt_exchange_message_bytes")(k_msg))
+    if len(raw) != need:  # the C side checks the same; fail before handing it a short buffer
+        raise BtError(f"exchange block holds {len(raw)} bytes, expected {need} "
+                      f"(world {world} x message of k_msg {k_msg})")
     out = np.zeros(max(k, 1), TOPK_DTYPE)
     cnt = np.zeros(2, np.int64)
-    m = _check(lib().bt_exchange_merge(raw.ctypes.data, world, k_msg, out.ctypes.data, k,
-                                       cnt.ctypes.data))
+    m = _check(sym("bt_exchange_merge")(raw.ctypes.data, len(raw), world, k_msg, out.ctypes.data,
+                                        k, cnt.ctypes.data))
     return out[:m], [int(cnt[0]), int(cnt[1])]
 
 

@@ -109,6 +109,8 @@ class Worker:
         # completions whose CompleteJob failed: (id, data, retry time, attempts)
         self._retry: list = []
         self.retry_base_s, self.retry_max_s = 0.25, 8.0
+        # shutdown: how long to wait for the compute thread, and per last CompleteJob attempt
+        self.stop_join_s, self.flush_timeout_s = 60.0, 5.0
         self._opts = [("grpc.max_receive_message_length", max_receive)]
         self.channel = grpc.insecure_channel(target, options=self._opts)
         u = self.channel.unary_unary
@@ -234,10 +236,15 @@ class Worker:
                 self._send_completions()
         finally:
             self.stop.set()
-            th.join(timeout=5)
+            # the compute thread finishes its batch first (a GPU batch takes seconds at most),
+            # so the flush below sees every completion it produces
+            th.join(timeout=self.stop_join_s)
             for f in fetch:
                 f.join(timeout=5)
             self._flush_retries()
+            if th.is_alive():
+                log.warning("Compute thread still running after %.0f s: completions of the batch "
+                            "it holds are not delivered by this worker", self.stop_join_s)
             self.channel.close()
 
     def _flush_retries(self):
@@ -253,8 +260,8 @@ class Worker:
                 break
         lost = []
         for jid, data, _, _ in pending:
-            try:
-                self._complete(P.CompleteRequest(id=jid, data=data))
+            try:  # bounded: a hung dispatcher must not block the worker's shutdown
+                self._complete(P.CompleteRequest(id=jid, data=data), timeout=self.flush_timeout_s)
             except grpc.RpcError:
                 lost.append(jid)
         if lost:

@@ -27,8 +27,9 @@ extern "C" {
 
 /* 2: bt_batch_profile.payload_bytes_read; the device top-k never overflows (bt_topk_fetch_wait
  *    and bt_exchange_wait return exact records on tie-heavy grids); bt_summary.hash is the
- *    additive trade hash of docs/oracle_spec.md §4 (version 1 hosts may hold FNV-1a hashes). */
-#define BT_ABI_VERSION 2
+ *    additive trade hash of docs/oracle_spec.md §4 (version 1 hosts may hold FNV-1a hashes).
+ * 3: bt_exchange_merge takes the gathered block's byte length and rejects a mismatch. */
+#define BT_ABI_VERSION 3
 
 typedef struct bt_engine bt_engine;
 
@@ -231,14 +232,15 @@ void bt_comm_destroy(bt_comm* c);
 int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot);
 int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
                          int64_t* counters);
-/* The host half of bt_exchange_wait, callable without a GPU: `block` holds `world` messages of
- * bt_exchange_message_bytes(k_msg) bytes in rank order, each [header record whose first int32 is
+/* The host half of bt_exchange_wait, callable without a GPU: `block` (block_bytes long, which
+ * must equal world * bt_exchange_message_bytes(k_msg), else -1) holds `world` messages in rank
+ * order, each [header record whose first int32 is
  * the record count n (clipped to k_msg; < 0 is an error) | k_msg records, the first n sorted |
  * int64 bar-evals | int64 trades], as the all-gather delivers them. Writes the min(k, k_msg,
  * sum n) best records in engine order and counters[2] = the summed counters; returns the count. */
 int64_t bt_exchange_message_bytes(int32_t k_msg);
-int32_t bt_exchange_merge(const uint8_t* block, int32_t world, int32_t k_msg, bt_topk_rec* out,
-                          int32_t k, int64_t* counters);
+int32_t bt_exchange_merge(const uint8_t* block, size_t block_bytes, int32_t world, int32_t k_msg,
+                          bt_topk_rec* out, int32_t k, int64_t* counters);
 
 /* ---- self-test hooks (host-side helpers the tests call without a GPU) */
 /* The CompleteRequest.data text of P summaries (spec §6, one JSON line per param), as

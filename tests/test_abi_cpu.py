@@ -40,7 +40,7 @@ def test_library_targets_gfx950_only():
 
 
 def test_abi_version_and_no_gpu_failure():
-    assert D.lib().bt_abi_version() == 2
+    assert D.lib().bt_abi_version() == 3
     try:
         import torch
         has_gpu = torch.cuda.is_available()
@@ -171,7 +171,7 @@ def test_c99_host_compiles_and_struct_layouts_match_the_python_mirror(tmp_path):
     (engine.py ctypes classes and numpy dtypes) reads has the header's size and offsets."""
     exe = build_abi_host(tmp_path)
     got = json.loads(subprocess.run([exe, "layout"], capture_output=True, text=True, check=True).stdout)
-    assert got["abi_version"] == 2
+    assert got["abi_version"] == 3
     mirror = {"bt_config": E._Config, "bt_job_in": E._JobIn, "bt_job_out": E._JobOut,
               "bt_batch_profile": E._BatchProfile, "bt_stats": E._Stats}
     for cname, cls in mirror.items():

@@ -58,7 +58,7 @@ def test_exchange_merge_matches_numpy_order(world, ties):
     parts = [_rank_records(rng, r, n, tie_vals) for r, n in enumerate(sizes)]
     counters = [(int(rng.integers(0, 2**40)), int(rng.integers(0, 2**30))) for _ in range(world)]
     block = _block(parts, k_msg, counters)
-    assert len(block) == world * E.lib().bt_exchange_message_bytes(k_msg)
+    assert len(block) == world * E.sym("bt_exchange_message_bytes")(k_msg)
     for k in (1, 7, k_msg, 3 * k_msg):
         got, cnt = E.exchange_merge(block, world, k_msg, k)
         exp = _engine_order(np.concatenate(parts))[:min(k, k_msg)]
@@ -88,6 +88,27 @@ def test_exchange_merge_rejects_a_negative_count():
     block = E.exchange_message(np.zeros(0, D.TOPK_DTYPE), 4, 0, 0) + bytes(msg)
     with pytest.raises(D.BtError, match="rank 1"):
         E.exchange_merge(block, 2, 4, 4)
+
+
+def test_exchange_merge_rejects_a_mismatched_block():
+    """A short block (a truncated gather) or one built for another k_msg is rejected by the C side
+    itself, not read past its end."""
+    import ctypes as C
+    k_msg = 4
+    one = E.exchange_message(np.zeros(0, D.TOPK_DTYPE), k_msg, 0, 0)
+    with pytest.raises(D.BtError, match="expected"):
+        E.exchange_merge(one * 2 + one[:-1], 3, k_msg, 4)         # Python wrapper check
+    with pytest.raises(D.BtError, match="expected"):
+        E.exchange_merge(one * 2, 2, k_msg + 1, 4)                # sent with another k
+    raw = np.frombuffer(one * 2, np.uint8)
+    out = np.zeros(4, D.TOPK_DTYPE)
+    cnt = np.zeros(2, np.int64)
+    for nbytes in (len(raw) - 1, len(raw) + 8, 0):                 # the C check alone
+        rc = E.sym("bt_exchange_merge")(raw.ctypes.data, nbytes, 2, k_msg, out.ctypes.data, 4,
+                                        cnt.ctypes.data)
+        assert rc == -1 and b"bytes" in E.lib().bt_last_error()
+    assert E.sym("bt_exchange_merge")(raw.ctypes.data, len(raw), 2, k_msg, out.ctypes.data, 4,
+                                      cnt.ctypes.data) == 0
 
 
 def test_libbt_does_not_link_rccl():

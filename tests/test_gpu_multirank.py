@@ -9,6 +9,7 @@ The reference's only parallelism is whole-file job farming (/root/reference/src/
 131-143); this checks the MI355X replacement's exchange step at world 2."""
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -37,12 +38,26 @@ def test_torchrun_two_ranks_exchange_equals_single_engine(config, extra):
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", str(config), "--steps", "2",
            "--warmup", "1", "--verify", "--no-cpu-baseline"] + extra
     env = dict(os.environ, OMP_NUM_THREADS="4")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    # its own session: on a timeout the whole group goes (the launcher AND its rank processes,
+    # which hold the GPU), not only the launcher
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT,
+                         env=env, start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=110)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        raise
+    assert p.returncode == 0, err[-3000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2
+    # per-rank attribution of a scaling loss
+    pr = d["per_rank"]
+    assert len(pr["kernel_avg_ms"]["by_rank"]) == 2 and pr["kernel_avg_ms"]["min"] > 0
+    assert len(pr["exchange_wait_ms_per_step"]["by_rank"]) == 2
+    assert sum(pr["symbols"]) == d["config"]["symbols_total"]
     assert "gloo all-gather" in d["config"]["parallelism"], d["config"]["parallelism"]
     v = d["verified_exchange"]
     assert v["topk"] == 100 and v["symbols"] == d["config"]["symbols_total"]

@@ -187,8 +187,10 @@ def test_pending_retries_get_a_last_attempt_and_a_log_on_stop(caplog):
     import grpc
     import logging
     sent = []
+    timeouts = []
 
-    def down(req):
+    def down(req, timeout=None):
+        timeouts.append(timeout)  # the last attempts are bounded
         if req.id == "j1":
             sent.append(req.id)
             return None
@@ -201,6 +203,7 @@ def test_pending_retries_get_a_last_attempt_and_a_log_on_stop(caplog):
         with caplog.at_level(logging.WARNING):
             w._flush_retries()
         assert sent == ["j1"] and not w._retry
+        assert timeouts == [w.flush_timeout_s] * 3 and w.flush_timeout_s > 0
         assert "2 completions undelivered" in caplog.text and "j2" in caplog.text and "j3" in caplog.text
     finally:
         w.channel.close()
