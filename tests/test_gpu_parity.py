@@ -466,6 +466,42 @@ def test_boll_sltp_level_sharing(sl, tp):
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
+def _zigzag(bars, seed):
+    """Closes alternating by ~0.1 % with wide wicks: with k = 0 and zero-bps stops every lane
+    trades every other bar (~21 trades per lane and tile)."""
+    rng = np.random.default_rng(seed)
+    base = 1_000_000 + np.cumsum(rng.integers(-50, 51, bars))
+    c = (base + np.where(np.arange(bars) % 2 == 0, 0, 1000)).astype(np.int64)
+    h = c + rng.integers(0, 3000, bars)
+    lo = c - rng.integers(0, 3000, bars)
+    return [x.astype(np.int32) for x in (h, lo, c)]
+
+
+@pytest.mark.parametrize("segments", [1, 3])
+def test_boll_trade_flood(segments):
+    """A grid and series that trade every other bar on every lane (~21 trades per lane and tile,
+    ~8,000 per block-tile: the finder's record buffer and the walkers' loops near their per-tile
+    maximum; split into bar segments too); every field vs the oracle."""
+    grid = D.Grid.boll([2, 3, 4, 5, 6, 7, 8, 9], [0, 1, 2, 3], [0, 1], [0, 1, 2, 3], k_den=4)
+    series = [_zigzag(3000, 1), _zigzag(2500, 2)]
+    with D.Engine(grid, parity=segments == 1, trade_cap=CAP if segments == 1 else 0) as e:
+        e.set_segments(segments)
+        e.load_ohlc([s[2] for s in series], [s[0] for s in series], [s[1] for s in series])
+        e.run()
+        got = e.summaries()
+        tr = e.trades() if segments == 1 else None
+        if segments > 1:
+            assert e.last_segments() == segments
+    for i, (h, lo, c) in enumerate(series):
+        orc, otr = oracle_row("boll", grid, (c, h, lo, c), 98280, CAP if segments == 1 else 0)
+        assert int(orc[0]["n_trades"]) > 600, orc[0]
+        for p in range(grid.n_params):
+            where = f"zigzag {i} {grid.param(p)}"
+            compare_summary(got[i, p], orc[p], where)
+            if tr is not None:
+                compare_trades(tr[i, p], otr[p], min(int(orc[p]["n_trades"]), CAP), where)
+
+
 def test_run_batch_binary_and_csv_mixed():
     """bt_run_batch on one JobsReply mixing DBXCOL1 payloads (decoded straight into the pinned
     staging rows), CSV text, and malformed payloads of every kind: good jobs bit-exact vs the
