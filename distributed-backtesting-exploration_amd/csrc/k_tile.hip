@@ -1447,7 +1447,9 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
             }
             __builtin_amdgcn_s_setprio(0);
         }
-        if (accountant && active && ka >= T_walk && ka < T_end && !BT_ABL(g, 8)) {
+        // (profiling: 4096 drops the accountant's records, an upper bound on what a cheaper
+        // accountant can gain)
+        if (accountant && active && ka >= T_walk && ka < T_end && !BT_ABL(g, 8) && !BT_ABL(g, 4096)) {
             // accountant: the finder's records of tile ka, in order (the tile's buffers stay
             // until step ka + 2: four stages, levels in three)
             set_prio(BT_PRIO(g, 18, kBollAcctPrio));

@@ -20,6 +20,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # BT_LIB (tuning aid): another in-tree build of the library, e.g. libbt_base.so for an A/B
 LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("BT_LIB", "libbt.so")))
 CSRC = os.path.join(PKG_DIR, "csrc")
+# include/bt.h BT_ABI_VERSION this wrapper is written against (build() checks the built library)
+ABI_VERSION = 3
 
 BT_SMA_CROSS, BT_EMA_OLS, BT_BOLL = 1, 2, 3
 BT_FLAG_PARITY, BT_FLAG_TIMING = 1, 2

@@ -40,7 +40,10 @@ def test_library_targets_gfx950_only():
 
 
 def test_abi_version_and_no_gpu_failure():
-    assert D.lib().bt_abi_version() == 3
+    hdr = open(os.path.join(ROOT, "include", "bt.h")).read()
+    want = int(re.search(r"#define BT_ABI_VERSION (\d+)", hdr).group(1))
+    # the header, the wrapper (and so __graft_entry__.build()'s check) and the library agree
+    assert D.lib().bt_abi_version() == D.ABI_VERSION == want
     try:
         import torch
         has_gpu = torch.cuda.is_available()

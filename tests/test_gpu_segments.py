@@ -219,14 +219,18 @@ def test_sma_split_tied_burn_in_takes_the_fix_pass():
     walk = lambda n, c0: np.clip(c0 + np.cumsum(rng.integers(-3000, 3001, n)), 10_000, 2**31 - 1)
     a = walk(5000, 1_000_000)
     c = np.concatenate([a, np.full(10000, a[-1]), walk(5000, a[-1])]).astype(np.int32)
-    cols = [(c, c, c, c)]
+    # a second symbol without flat stretches: its boundaries agree while the first symbol's
+    # re-walk, so the fix pass must leave the agreeing symbol's segments as they are
+    c2 = walk(20000, 2_000_000).astype(np.int32)
+    cols = [(c, c, c, c), (c2, c2, c2, c2)]
     ref, _, _ = _run_grid(grid, cols, 1)
     got, used, refixed = _run_grid(grid, cols, 3, 1)   # boundaries at bars 6,720 and 13,376
     assert used == 3 and refixed > 0
     assert got.tobytes() == ref.tobytes()
-    orc, _ = oracle_row("sma", grid, (c, c, c, c), 98280)
-    for p in range(grid.n_params):
-        compare_summary(got[0, p], orc[p], f"sma flat boundary {grid.param(p)}")
+    for i, x in enumerate((c, c2)):
+        orc, _ = oracle_row("sma", grid, (x, x, x, x), 98280)
+        for p in range(grid.n_params):
+            compare_summary(got[i, p], orc[p], f"sma flat boundary sym {i} {grid.param(p)}")
 
 
 def test_sma_auto_segments_only_for_few_long_blocks():
