@@ -1386,16 +1386,18 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 // close, 2 low-level fill, 3 high-level fill)
                 uint16_t* RB = recs + (k & 1) * kRecCap * kTile + lane;
                 int nr = 0, fcur = 0;
-                bool first = true;  // wave-uniform: only the first trade can start open
-#pragma unroll 1
-                while (true) {
+                // one trade per call, false when the lane's tile is done; the first call of the
+                // tile is peeled (FIRST: only it can start open and search with the carried
+                // levels), so the loop's body has no branch on it
+                auto find = [&](auto first_tag) -> bool {
+                    constexpr bool FIRST = decltype(first_tag)::value;
                     if (STAMPS) sa.count(3);
                     int xlo = kTile, xhi = kTile;
                     bool entered = false;
                     uint32_t rec;
-                    if (!first || fpos == 0) {
+                    if (!FIRST || fpos == 0) {
                         const uint64_t m = (ZL | ZH) & bits_from(fcur);
-                        if (m == 0) break;
+                        if (m == 0) return false;
                         const int b = __builtin_ctzll(m);
                         const int np = ((ZL >> b) & 1) ? 1 : -1;
                         const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
@@ -1421,7 +1423,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         const bool lg = fpos > 0;
                         const uint64_t sig = (lg ? DP : DN) & (~0ULL << fcur);
                         x = sig ? __builtin_ctzll(sig) : kTile;
-                        if (first && !entered) sltp_search(LO, fcur, XL, XHm1, xlo, xhi);
+                        if (FIRST && !entered) sltp_search(LO, fcur, XL, XHm1, xlo, xhi);
                         const int xs = min(xlo, xhi);
                         const bool hit = xs < kTile && xs <= x;
                         if (hit) x = xs;
@@ -1437,10 +1439,15 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         RB[nr * kTile] = (uint16_t)rec;
                         ++nr;
                     }
-                    if (!more) break;
+                    if (!more) return false;
                     fpos = 0;
                     fcur = x + 1;
-                    first = false;
+                    return true;
+                };
+                if (find(std::true_type{})) {
+#pragma unroll 1
+                    while (find(std::false_type{})) {
+                    }
                 }
                 nrec[(k & 1) * kTile + lane] = (uint8_t)nr;
                 if (STAMPS) sa.mark(1);
