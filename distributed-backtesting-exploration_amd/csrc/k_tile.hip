@@ -1474,12 +1474,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 constexpr bool NARROW = decltype(narrow_tag)::value;
                 // gap, mdd (SEG: the forms) within 2 TV < 2^31 if NARROW
                 Acct32 n32{(int32_t)a.gap, (int32_t)a.mdd};
-#pragma unroll 1
-                for (int i = 0; i < n; ++i) {
+                // one record per call; the tile's first is peeled (FIRST: only it can be the exit
+                // of a position carried in), so every later record enters at b
+                auto record = [&](auto first_tag, int i) {
+                    constexpr bool FIRST = decltype(first_tag)::value;
                     if (STAMPS) sa.count(3);
                     const uint32_t rec = RB[i * kTile];
                     const int b = (int)(rec & 63u), x = (int)((rec >> 8) & 63u), kind = (int)(rec >> 14);
-                    if (rec & 64u) {  // entry at b
+                    if (!FIRST || (rec & 64u)) {  // entry at b
                         const int np = (rec & 128u) ? 1 : -1;
                         const int rl = (np > 0 ? lev_lo_long : lev_lo_short) * kTile + b;
                         const int rh = (np > 0 ? lev_hi_long : lev_hi_short) * kTile + b;
@@ -1497,13 +1499,19 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                     if (kind != 0) {  // exit at x
                         const bool hit = kind >= 2;
                         const int qi = hit ? x - 1 : x;
-                        const Agg seg = dst_query_w(D, a.sb, max(qi, a.sb));
+                        // (a later record's exit follows its entry bar a.sb: qi >= a.sb)
+                        const Agg seg = dst_query_w(D, a.sb, FIRST ? max(qi, a.sb) : qi);
                         const int32_t cxx = cT[x];
                         const int64_t qx = ql[x], q2x = ql[kTile + x];
                         asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
                         const int32_t px = hit ? (kind == 2 ? XL : XHm1 + 1) : cxx;
                         close_trade(narrow_tag, n32, ta, x, qi, px, seg, qx, q2x);
                     }
+                };
+                if (n > 0) {
+                    record(std::true_type{}, 0);
+#pragma unroll 1
+                    for (int i = 1; i < n; ++i) record(std::false_type{}, i);
                 }
                 if (NARROW) {
                     a.gap = (uint32_t)n32.g;  // >= 0

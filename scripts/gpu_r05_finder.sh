@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: the Bollinger finder's first trade of a tile peeled out of its loop (libbt.so) vs the
+# Round 5: (current Bollinger change: libbt.so) vs the
 # same source without (libbt_base.so): Bollinger parity, then config 4 kernel time, interleaved.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r05/finder
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
