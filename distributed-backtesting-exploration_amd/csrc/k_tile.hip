@@ -1065,37 +1065,13 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
         const uint64_t tin = ballot(t < B);  // bars of the tile inside the series
         const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
+        // window tasks (counter values [0, nw)) first, then level tasks: a wave's grabs only
+        // grow, so two loops, each body one kind of task
 #pragma unroll 1
-        while (o < (uint32_t)ntask) {
+        while (o < (uint32_t)nw) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
-            const int ow = (int)o, ol = ow - nw;  // window task ow, or level task ol
+            const int ow = (int)o;
             const uint64_t tt0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-            if (ol >= 0) {  // level task: lane = entry bar b, first passage from b + 1
-                const int side = ol & 1, i = ol >> 1 << kLevPassLog;
-                const int32_t* LH = lhs_ + s * kLH;
-                const double cd = (double)c;
-                uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
-                int32_t* ptab = levp + ((T % 3) * 2 + side) * nlev * kTile;
-                // kLevPass levels: independent searches, all stored after all
-                {
-                    int x[kLevPass];
-                    int32_t X[kLevPass];
-#pragma unroll
-                    for (int u = 0; u < kLevPass; ++u) {
-                        const double y = level_y(cd, levf[side * nlev + min(i + u, nu - 1)]);
-                        X[u] = side == 0 ? (int32_t)y : (y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
-                        x[u] = side == 0 ? first_low(LH, lane + 1, X[u]) : first_high(LH, lane + 1, X[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kLevPass; ++u) {
-                        tab[min(i + u, nu - 1) * kTile + lane] = (uint8_t)x[u];
-                        ptab[min(i + u, nu - 1) * kTile + lane] = X[u];
-                    }
-                }
-                if (STAMPS) sa.task[1] += __builtin_amdgcn_s_memtime() - tt0;
-                o = grab_value(vn) - base;
-                continue;
-            }
             const int Wn = nw <= 64 ? __builtin_amdgcn_readlane(winreg, ow & 63) : win[ow];
             const int jj = t + 1 - Wn;
             const bool valid = jj >= 0 && t < B;
@@ -1183,6 +1159,35 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                 Wd[nw * nk + 2 * ow + 1] = dn;
             }
             if (STAMPS) sa.task[0] += __builtin_amdgcn_s_memtime() - tt0;
+            o = grab_value(vn) - base;
+        }
+#pragma unroll 1
+        while (o < (uint32_t)ntask) {  // level task: lane = entry bar b, first passage from b + 1
+            const uint32_t vn = grab_issue(ctr, lane);
+            const int ol = (int)o - nw;
+            const uint64_t tt0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+            const int side = ol & 1, i = ol >> 1 << kLevPassLog;
+            const int32_t* LH = lhs_ + s * kLH;
+            const double cd = (double)c;
+            uint8_t* tab = levt + ((T & 1) * 2 + side) * nlev * kTile;
+            int32_t* ptab = levp + ((T % 3) * 2 + side) * nlev * kTile;
+            // kLevPass levels: independent searches, all stored after all
+            {
+                int x[kLevPass];
+                int32_t X[kLevPass];
+#pragma unroll
+                for (int u = 0; u < kLevPass; ++u) {
+                    const double y = level_y(cd, levf[side * nlev + min(i + u, nu - 1)]);
+                    X[u] = side == 0 ? (int32_t)y : (y >= 2147483648.0 ? INT32_MAX : (int32_t)y - 1);
+                    x[u] = side == 0 ? first_low(LH, lane + 1, X[u]) : first_high(LH, lane + 1, X[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kLevPass; ++u) {
+                    tab[min(i + u, nu - 1) * kTile + lane] = (uint8_t)x[u];
+                    ptab[min(i + u, nu - 1) * kTile + lane] = X[u];
+                }
+            }
+            if (STAMPS) sa.task[1] += __builtin_amdgcn_s_memtime() - tt0;
             o = grab_value(vn) - base;
         }
     };
