@@ -357,8 +357,9 @@ void run_impl(bt_engine* e) {
     out.n_trades = e->ntr[b];
     out.dbg = nullptr;
     if (BT_ABL(e->grid, 64)) {  // profiling stamps (profiling build only)
-        e->d_dbg.ensure(80);
-        HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, 80 * sizeof(unsigned long long), e->stream));
+        e->d_dbg.ensure(kDbgSlots + 8 * kDbgBlocks);
+        HIPCHK(hipMemsetAsync(e->d_dbg.p, 0, (kDbgSlots + 8 * kDbgBlocks) * sizeof(unsigned long long),
+                              e->stream));
         out.dbg = e->d_dbg.p;
     }
     const bool timing = (e->cfg.flags & BT_FLAG_TIMING) != 0;
@@ -1104,7 +1105,7 @@ int32_t bt_read_close(bt_engine* e, int32_t sym_index, int32_t* out, int32_t n) 
 
 int32_t bt_read_debug(bt_engine* e, uint64_t* out, int32_t n) {
     ABI_GUARD(-1, {
-        if (!e || !out || n < 0 || n > 80 || !e->d_dbg.p) throw HipFail{"no debug stamps"};
+        if (!e || !out || n < 0 || n > kDbgSlots + 8 * kDbgBlocks || !e->d_dbg.p) throw HipFail{"no debug stamps"};
         activate(e);
         sync_all(e);
         HIPCHK(hipMemcpy(out, e->d_dbg.p, (size_t)n * 8, hipMemcpyDeviceToHost));

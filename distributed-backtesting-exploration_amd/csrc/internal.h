@@ -18,6 +18,9 @@
 #define BT_ABL(g, bit) false
 #define BT_PRIO(g, shift, dflt) (dflt)
 #endif
+// profiling stamps: slots [0, 80) role cycles, then where each of the first kDbgBlocks blocks'
+// first 8 waves ran (HW_ID | XCC_ID << 32 | 1 << 40)
+constexpr int kDbgSlots = 80, kDbgBlocks = 1024;
 
 namespace bt {
 

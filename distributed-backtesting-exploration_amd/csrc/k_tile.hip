@@ -255,6 +255,17 @@ __device__ __forceinline__ uint64_t latch64(uint64_t S, uint64_t R, uint64_t q) 
 
 }  // namespace
 
+// profiling stamps: the hardware placement (SE / CU / SIMD, XCD) of wave hw_wave < 8 of the
+// first kDbgBlocks blocks (internal.h)
+__device__ __forceinline__ void stamp_place(unsigned long long* dbg, int hw_wave, int lane) {
+    if (dbg == nullptr || lane != 0 || hw_wave >= 8 || blockIdx.x >= (unsigned)kDbgBlocks || blockIdx.y != 0 ||
+        blockIdx.z != 0)
+        return;
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // XCC_ID
+    dbg[kDbgSlots + blockIdx.x * 8 + hw_wave] = ((unsigned long long)xcc << 32 | hw) | (1ull << 40);
+}
+
 // ----------------------------------------------------------------------------- EMA + OLS
 // Workgroup = parameter waves + helper A + helper B, one barrier per tile:
 //   helper A, tile k+2: closes -> returns, drawdown sparse table, prefix rings;
@@ -328,6 +339,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             if (tid == 0) atomicAdd(sg.refixed, 1ULL);
         }
     }
+    if (STAMPS) stamp_place(out.dbg, wave, lane);
     const int T_scan = sr.T_scan, T_walk = sr.T_walk, T_acct = sr.T_acct, T_end = sr.T_end;
     // the chains start at bar 0 with e = c there; a speculative segment's chains continue from
     // an estimate of the true values entering its first scanned bar, and the fix pass starts
@@ -865,6 +877,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // indices), so the heavy roles land on different SIMDs next to light ones
     const int tid = threadIdx.x, lane = tid & 63, hw_wave = tid >> 6;
     const int wave = hw_wave < 8 ? (int)((wave_map >> (4 * hw_wave)) & 15u) : hw_wave;
+    if (STAMPS) stamp_place(out.dbg, hw_wave, lane);
     // waves: [0, npw) parameter groups, npw the helper, npw + 1 .. npw + nsplit the accountants
     // of a split walk, then `nextra` task-only waves. Without a split every parameter wave walks
     // and accounts its lanes' trades (walker); with one, parameter wave split_grp (the group of
