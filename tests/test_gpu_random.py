@@ -19,6 +19,7 @@ CAP = 4096
 # seeds per sweep (BT_RANDOM_SEEDS widens a sweep for a one-off deep run); the defaults are
 # sized so the driver's round-end `-m gpu` run carries a few hundred random cases (~10 s)
 NS = int(os.environ.get("BT_RANDOM_SEEDS", "0"))
+S0 = int(os.environ.get("BT_RANDOM_SEED0", "0"))  # first seed of a deep run (fresh seeds)
 
 
 def _series(rng, n, kind):
@@ -44,7 +45,7 @@ def _windows(rng, k, top):
     return sorted(set(int(x) for x in rng.integers(1, top, k)))
 
 
-@pytest.mark.parametrize("seed", range(NS or 120))
+@pytest.mark.parametrize("seed", range(S0, S0 + (NS or 120)))
 def test_random_sma(seed):
     rng = np.random.default_rng(1000 + seed)
     grid = D.Grid.sma(_windows(rng, 7, 40), _windows(rng, 6, 300), annualization=252)
@@ -63,7 +64,7 @@ def test_random_sma(seed):
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
-@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("ema_ols", "boll") for s in range(NS or 40)])
+@pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("ema_ols", "boll") for s in range(S0, S0 + (NS or 40))])
 def test_random_tile_strategies(strategy, seed):
     rng = np.random.default_rng(2000 + seed + (100 if strategy == "boll" else 0))
     if strategy == "ema_ols":
@@ -90,7 +91,7 @@ def test_random_tile_strategies(strategy, seed):
 
 
 @pytest.mark.parametrize("strategy,seed", [(st, s) for st in ("sma", "ema_ols", "boll")
-                                           for s in range(NS or 40)])
+                                           for s in range(S0, S0 + (NS or 40))])
 def test_random_product_kernels(strategy, seed):
     """The release instantiations (no trade lists: the split Bollinger walk, the SMA kernel's
     fast paths) on the same kinds of random grids and paths, every summary field vs the oracle."""
