@@ -7,8 +7,8 @@ before timing. One step = one pass of the hot path over that batch: the fused st
 (indicators + signals + position/PnL/drawdown/Sharpe per lane), the per-GPU top-k and its
 read-back; for N > 1 also the exchange step: ONE RCCL all-gather of every
 rank's top-k records and counters, issued through the C ABI (bt_exchange_async, csrc/comm.cpp)
-straight from the engine's device buffers. Step i+1 is enqueued before step i's read-back /
-exchange is consumed, so host work and the collective overlap the next pass.
+straight from the engine's device buffers. Step i+1 (at N > 1 also step i+2) is enqueued before
+step i's read-back / exchange is consumed, so host work and the collective overlap the next pass.
 
 `--config 3|4|5` runs BASELINE's other configs with STRONG scaling by default: the pinned
 totals (config 3: 500 symbols x 98,280 1-min bars x 64 params, quoted at 1 and 2 GPUs; config 4:
@@ -228,40 +228,57 @@ def main():
         if comm is None:
             exchange = f"{dist.get_backend()} all-gather via torch.distributed"
 
+    # steps in flight ahead of the one being consumed: at N > 1 two, so step i+2 is already
+    # enqueued when finish(i) blocks. A step's top-k chain gets CU slots only once the next
+    # step's kernel drains (config 4: persistent blocks hold every CU's LDS), so finish(i)
+    # returns about when kernel i+1 ends; one step ahead would leave the GPU idle for the
+    # exchange, the host merge and the next launch. N = 1 keeps one.
+    depth = 2 if world > 1 else 1
+    assert depth < D.PIPE_SLOTS
+
     def issue(i):
         eng.run()                      # kernels of step i, enqueued on the engine stream
         if topk == 0:
             return
+        slot = i % D.PIPE_SLOTS
         if comm is not None:
-            comm.exchange_async(eng, i & 1)   # RCCL all-gather behind the run's top-k chain
+            comm.exchange_async(eng, slot)   # RCCL all-gather behind the run's top-k chain
         else:
-            eng.topk_fetch_async(i & 1)       # its top-k + trade count into pinned slot i % 2
+            eng.topk_fetch_async(slot)       # its top-k + trade count into a pinned slot
+
+    xch_s = [0.0]  # host time in the torch.distributed exchange proper (all-gather + merge)
 
     def finish(i):
         """(top-k, [bar-evals, trades]) of step i over every rank."""
         if topk == 0:
             return None, None
+        slot = i % D.PIPE_SLOTS
         if comm is not None:
-            return comm.exchange_wait(i & 1)
-        top, trades = eng.topk_fetch_wait(i & 1)
+            return comm.exchange_wait(slot)
+        top, trades = eng.topk_fetch_wait(slot)
         if dist is None:
             return top, [n_sym * BARS * P, trades]
         # the one exchange step: a single all-gather carrying each rank's k x 24 B top-k records
         # and its run counters (summed on the host), in the C-ABI exchange's byte format
-        return PAR.exchange(top, topk, [n_sym * BARS * P, trades], dist)
+        tx = time.perf_counter()
+        r = PAR.exchange(top, topk, [n_sym * BARS * P, trades], dist)
+        xch_s[0] += time.perf_counter() - tx
+        return r
 
-    wait_s = [0.0]  # host time blocked in finish() (the read-back / exchange wait) this run
+    wait_s = [0.0]  # host time blocked in finish() this run: the wait for the step's GPU work
+                    # (kernel, top-k chain, read-back or RCCL all-gather) plus the exchange
 
     def steps(n):
-        """n steps; step i+1 is enqueued before step i's read-back and exchange, so the GPU runs
-        the next pass while the host consumes (and, for N > 1, exchanges) this one."""
+        """n steps; steps i+1 .. i+depth are enqueued before step i's read-back and exchange,
+        so the GPU runs the next passes while the host consumes (and, for N > 1, exchanges)
+        this one."""
         res = (None, None)
-        wait_s[0] = 0.0
-        if n > 0:
-            issue(0)
+        wait_s[0] = xch_s[0] = 0.0
+        for i in range(min(depth, n)):
+            issue(i)
         for i in range(n):
-            if i + 1 < n:
-                issue(i + 1)
+            if i + depth < n:
+                issue(i + depth)
             tw = time.perf_counter()
             res = finish(i)
             wait_s[0] += time.perf_counter() - tw
@@ -285,12 +302,19 @@ def main():
     per_rank = None
     if dist is not None:
         # max over ranks of the timed region; and, gathered once after it, every rank's own
-        # kernel average (HIP events) and host wait for the read-back / exchange per step, so a
-        # scaling loss can be told apart: load imbalance (kernel times differ) vs the exchange
-        # (kernel times equal, waits grow)
+        # kernel average (HIP events), its host wait in finish() per step, the exchange proper
+        # (torch.distributed carrier: all-gather + merge once the rank's top-k is on the host;
+        # the RCCL all-gather runs on the GPU's top-k stream instead, -1 here) and the kernel
+        # stream's idle time per step (timed region / steps - kernel average: what the exchange,
+        # the host merge and the launches cost the GPU; meaningless when ranks share a device),
+        # so a scaling loss can be told apart: load imbalance (kernel times differ) vs the exchange
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        mine = torch.tensor([elapsed, kms / max(launches, 1), wait_s[0] * 1e3 / max(args.steps, 1),
-                             float(n_sym)], dtype=torch.float64, device=dev)
+        k_avg = kms / max(launches, 1)
+        mine = torch.tensor([elapsed, k_avg, wait_s[0] * 1e3 / max(args.steps, 1),
+                             float(n_sym),
+                             xch_s[0] * 1e3 / max(args.steps, 1) if comm is None else -1.0,
+                             elapsed * 1e3 / max(args.steps, 1) - k_avg],
+                            dtype=torch.float64, device=dev)
         alls = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(alls, mine)
         rows = torch.stack(alls).cpu().numpy()
@@ -299,7 +323,11 @@ def main():
         def mm(col):
             return {"min": float(rows[:, col].min()), "max": float(rows[:, col].max()),
                     "by_rank": [float(x) for x in rows[:, col]]}
-        per_rank = {"kernel_avg_ms": mm(1), "exchange_wait_ms_per_step": mm(2),
+        per_rank = {"kernel_avg_ms": mm(1), "host_wait_ms_per_step": mm(2),
+                    "exchange_ms_per_step": mm(4) if comm is None else None,
+                    "gpu_idle_ms_per_step": mm(5),
+                    "ranks_share_device": torch.cuda.device_count() < world,
+                    "pipeline_depth": depth,
                     "timed_region_s": mm(0), "symbols": [int(x) for x in rows[:, 3]]}
     stats = eng.stats()
     # bar segments per symbol of the last run and the blocks its fix passes re-walked (read

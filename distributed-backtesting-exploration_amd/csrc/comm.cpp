@@ -7,7 +7,7 @@
 // contiguous block of symbols with no data-path collective; once per run the ranks exchange
 // [header record | k records | bar-evals | trades] (k = 100: 2.4 KB per rank). That message is
 // latency-bound, so it is a single ncclAllGather on the engine's top-k stream, enqueued behind
-// the run's top-k chain without a host wait, and read back into one of two pinned slots so the
+// the run's top-k chain without a host wait, and read back into one of BT_PIPE_SLOTS pinned slots so the
 // next run overlaps it (the same pipelining as bt_topk_fetch_async / bt_topk_fetch_wait).
 //
 // RCCL is resolved with dlopen on the first communicator call, not linked: a single-GPU worker
@@ -35,11 +35,11 @@ struct bt_comm {
     int32_t rank = 0, world = 1, device = 0, k = 0;
     size_t rec_bytes = 0;              // bytes one rank contributes
     unsigned char* d_send = nullptr;   // [rec_bytes]
-    unsigned char* d_recv[2] = {nullptr, nullptr};  // [world * rec_bytes] per slot
-    unsigned char* h_recv[2] = {nullptr, nullptr};  // pinned
-    int64_t* h_evals[2] = {nullptr, nullptr};       // pinned: this rank's bar-evals per slot
-    hipEvent_t done[2] = {nullptr, nullptr};
-    bool armed[2] = {false, false};
+    unsigned char* d_recv[BT_PIPE_SLOTS] = {};  // [world * rec_bytes] per slot
+    unsigned char* h_recv[BT_PIPE_SLOTS] = {};  // pinned
+    int64_t* h_evals[BT_PIPE_SLOTS] = {};       // pinned: this rank's bar-evals per slot
+    hipEvent_t done[BT_PIPE_SLOTS] = {};
+    bool armed[BT_PIPE_SLOTS] = {};
 };
 
 namespace {
@@ -143,12 +143,12 @@ int32_t merge_block(const unsigned char* block, int32_t world, int32_t k_msg, bt
 void release(bt_comm* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BT_PIPE_SLOTS; ++s) {
         if (c->done[s]) (void)hipEventSynchronize(c->done[s]);
     }
     if (c->comm) (void)rccl().CommDestroy(c->comm);  // comm set: rccl() resolved
     if (c->d_send) (void)hipFree(c->d_send);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BT_PIPE_SLOTS; ++s) {
         if (c->d_recv[s]) (void)hipFree(c->d_recv[s]);
         if (c->h_recv[s]) (void)hipHostFree(c->h_recv[s]);
         if (c->h_evals[s]) (void)hipHostFree(c->h_evals[s]);
@@ -196,7 +196,7 @@ bt_comm* bt_comm_create(const uint8_t* id, int32_t rank, int32_t world, int32_t 
         memcpy(&uid, id, sizeof uid);
         NCCLCHK(nc.CommInitRank(&c->comm, world, uid, rank));
         HIPCHK(hipMalloc(&c->d_send, c->rec_bytes));
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < BT_PIPE_SLOTS; ++s) {
             HIPCHK(hipMalloc(&c->d_recv[s], c->rec_bytes * world));
             HIPCHK(hipHostMalloc(&c->h_recv[s], c->rec_bytes * world));
             HIPCHK(hipHostMalloc(&c->h_evals[s], sizeof(int64_t)));
@@ -220,7 +220,7 @@ void bt_comm_destroy(bt_comm* c) { release(c); }
 
 int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot) {
     try {
-        if (!c || !e || slot < 0 || slot > 1) throw CommFail{"bad arguments"};
+        if (!c || !e || slot < 0 || slot >= BT_PIPE_SLOTS) throw CommFail{"bad arguments"};
         ExchangeView v{};
         std::string why;
         if (!engine_exchange_view(e, v, why)) throw CommFail{why};
@@ -257,7 +257,7 @@ int32_t bt_exchange_async(bt_comm* c, bt_engine* e, int32_t slot) {
 int32_t bt_exchange_wait(bt_comm* c, int32_t slot, bt_topk_rec* out, int32_t k,
                          int64_t* counters) {
     try {
-        if (!c || slot < 0 || slot > 1 || !out || k < 1) throw CommFail{"bad arguments"};
+        if (!c || slot < 0 || slot >= BT_PIPE_SLOTS || !out || k < 1) throw CommFail{"bad arguments"};
         if (!c->armed[slot]) throw CommFail{"no exchange pending on this slot"};
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipEventSynchronize(c->done[slot]));

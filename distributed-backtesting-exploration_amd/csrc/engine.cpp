@@ -120,9 +120,9 @@ struct bt_engine {
     DevBuf<bt_topk_rec> d_top;
     bt_topk_rec* h_top = nullptr;     // pinned host copy of d_top
     // pipelined read-back slots: header + kTopkMax records + one record holding the trade count
-    bt_topk_rec* h_slot[2] = {nullptr, nullptr};
-    hipEvent_t slot_ev[2] = {nullptr, nullptr};
-    bool slot_armed[2] = {false, false};
+    bt_topk_rec* h_slot[BT_PIPE_SLOTS] = {};
+    hipEvent_t slot_ev[BT_PIPE_SLOTS] = {};
+    bool slot_armed[BT_PIPE_SLOTS] = {};
     bool topk_ready = false;          // top-k buffers allocated and their state initialised
     bool ran = false;
     // timing of the dominant kernel
@@ -219,7 +219,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
                 e->grid.kn2[q] = (double)(kn * kn);  // exact: kn <= 2^20
             }
             e->grid.kmin_idx = (int32_t)(std::min_element(e->ax[1].begin(), e->ax[1].end()) - e->ax[1].begin());
-            if (boll_lds_bytes(e->grid, 1) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
+            if (boll_lds_bytes(e->grid) > 160 * 1024) return "Bollinger grid needs more LDS than a CU has (windows too long)";
             break;
         }
         default:
@@ -868,7 +868,7 @@ void bt_engine_destroy(bt_engine* e) {
         e->d_top.release();
         if (e->h_top) (void)hipHostFree(e->h_top);
         e->h_top = nullptr;
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < BT_PIPE_SLOTS; ++i) {
             if (e->h_slot[i]) (void)hipHostFree(e->h_slot[i]);
             if (e->slot_ev[i]) (void)hipEventDestroy(e->slot_ev[i]);
             e->h_slot[i] = nullptr;
@@ -1029,7 +1029,7 @@ int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k) {
 
 int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot) {
     ABI_GUARD(-1, {
-        if (!e || slot < 0 || slot > 1) throw HipFail{"bad arguments"};
+        if (!e || slot < 0 || slot >= BT_PIPE_SLOTS) throw HipFail{"bad arguments"};
         if (!e->ran || e->cfg.topk <= 0) throw HipFail{"top-k not computed (topk == 0 or no run)"};
         activate(e);
         if (!e->h_slot[slot])
@@ -1052,7 +1052,7 @@ int32_t bt_topk_fetch_async(bt_engine* e, int32_t slot) {
 int32_t bt_topk_fetch_wait(bt_engine* e, int32_t slot, bt_topk_rec* out, int32_t k,
                            int64_t* n_trades) {
     ABI_GUARD(-1, {
-        if (!e || slot < 0 || slot > 1 || !out || k <= 0) throw HipFail{"bad arguments"};
+        if (!e || slot < 0 || slot >= BT_PIPE_SLOTS || !out || k <= 0) throw HipFail{"bad arguments"};
         if (!e->slot_armed[slot]) throw HipFail{"no fetch pending on this slot"};
         activate(e);
         HIPCHK(hipEventSynchronize(e->slot_ev[slot]));

@@ -142,8 +142,7 @@ int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
 constexpr int kSmaBurnTiles = 2;
 int device_cus();  // compute units of the current device
 size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
-// dynamic LDS of the Bollinger tile kernel with nsplit finder/accountant pairs (1 or 2)
-size_t boll_lds_bytes(const Grid& g, int nsplit = 2);
+size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, const SegArgs& seg, hipStream_t st);
 // EMA+OLS segments: count for this shard (auto mode) and the burn-in a speculative segment needs

@@ -84,9 +84,8 @@ struct TileLds {
 };
 
 // kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
-// per side: nsl + ntp; nsplit finder / accountant pairs of a split walk, 1 or 2)
-__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0,
-                                                  int nsplit = 1) {
+// per side: nsl + ntp)
+__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0) {
     TileLds L{};
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
@@ -105,9 +104,9 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.levp = take((size_t)3 * 2 * nlev * kTile * 4);  // the levels (int32), [tile % 3][side][level][bar]
         L.levf = take((size_t)2 * nlev * 8);         // level factors per side
         L.lvb = take((size_t)(nlev + 1) * 4);        // distinct SL/TP bps, then their count
-        // trade records [pair][tile & 1][record][lane] and records per lane [pair][tile & 1][lane]
-        L.rec = take((size_t)nsplit * 2 * kRecCap * kTile * 2);
-        L.nrec = take((size_t)nsplit * 2 * kTile);
+        // the finder's trade records [tile & 1][record][lane] and records per lane [tile & 1][lane]
+        L.rec = take((size_t)2 * kRecCap * kTile * 2);
+        L.nrec = take((size_t)2 * kTile);
         L.nar = take((size_t)ns * 4);  // per tile stage: the accountant's sums fit int32 (Acct32)
     } else {
         L.ebuf = take((size_t)2 * na * kEStride * 8);
@@ -835,13 +834,14 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                                                          const int32_t* __restrict__ close,
                                                          Grid g, Out out, int nextra, int lpw,
                                                          SegArgs sg, int fix_seg, int split_grp,
-                                                         int split_grp2, uint32_t wave_map) {
+                                                         uint32_t wave_map) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = g.na, nk = g.nb, R = g.ring;
     const int nsl = g.nc, ntp = g.nd, nlev = nsl + ntp;
-    // finder / accountant pairs: parameter groups split_grp and (if >= 0) split_grp2
-    const int nsplit = split_grp < 0 ? 0 : (split_grp2 < 0 ? 1 : 2);
-    const TileLds LL = tile_lds_layout(1, R, nw, nk, nlev, nsplit > 0 ? nsplit : 1);
+    // a split walk: parameter group split_grp (>= 0) finds its trades, an accountant wave keeps
+    // their accounts
+    const bool split = split_grp >= 0;
+    const TileLds LL = tile_lds_layout(1, R, nw, nk, nlev);
     // prefix rings as exact doubles (every prefix < 2^53 for series up to kMaxBars = 2^22 bars):
     // sum c, and sum c^2 split at bit 31 into sum (c^2 >> 31) and sum (c^2 & (2^31 - 1)), so
     // a window's S1 and the two halves of S2 are exact double differences and S2 = hi 2^31 + lo
@@ -878,24 +878,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     const int tid = threadIdx.x, lane = tid & 63, hw_wave = tid >> 6;
     const int wave = hw_wave < 8 ? (int)((wave_map >> (4 * hw_wave)) & 15u) : hw_wave;
     if (STAMPS) stamp_place(out.dbg, hw_wave, lane);
-    // waves: [0, npw) parameter groups, npw the helper, npw + 1 .. npw + nsplit the accountants
-    // of a split walk, then `nextra` task-only waves. Without a split every parameter wave walks
-    // and accounts its lanes' trades (walker); with one, parameter wave split_grp (the group of
-    // the busiest z threshold, whose per-lane trade chain sets the tile time) only finds its
-    // trades (finder) and the accountant wave keeps their accounts, one tile behind; with two,
-    // the group of the second-busiest threshold (split_grp2) is split the same way.
-    const bool split = nsplit > 0;
-    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra - nsplit;
+    // waves: [0, npw) parameter groups, npw the helper, npw + 1 the accountant of a split walk,
+    // then `nextra` task-only waves. Without a split every parameter wave walks and accounts its
+    // lanes' trades (walker); with one, parameter wave split_grp (the group of the busiest z
+    // threshold, whose per-lane trade chain sets the tile time) only finds its trades (finder)
+    // and the accountant wave keeps their accounts, one tile behind.
+    const int nwaves = (int)(blockDim.x >> 6), npw = nwaves - 1 - nextra - (split ? 1 : 0);
     const bool helper = wave == npw;
-    const int acc_i = wave - npw - 1;
-    const bool accountant = split && acc_i >= 0 && acc_i < nsplit;
-    const int fin_i = wave == split_grp ? 0 : (wave == split_grp2 ? 1 : -1);
-    const bool finder = split && fin_i >= 0;
-    const int grp = accountant ? (acc_i == 0 ? split_grp : split_grp2) : wave;
-    // this wave's record buffers (finder and accountant of one pair share them)
-    const int pair = accountant ? acc_i : (finder ? fin_i : 0);
-    recs += (size_t)pair * 2 * kRecCap * kTile;
-    nrec += (size_t)pair * 2 * kTile;
+    const bool accountant = split && wave == npw + 1;
+    const bool finder = split && wave == split_grp;
+    const int grp = accountant ? split_grp : wave;
     const SymDesc sd = syms[blockIdx.x];
     const int B = sd.bars, ntiles = (B + kTile - 1) / kTile, P = g.n_params;
     const int j = (blockIdx.y * npw + grp) * lpw + lane;
@@ -1631,19 +1623,16 @@ static int tile_param_waves(int need, int cap) {
 // runs on SIMD w % 4, so waves w and w + 4 share one: each busy parameter wave (the walks, the
 // busiest first) gets a task-only wave as its partner (task waves take fewer tasks when their
 // SIMD is busy), the lightest parameter wave the helper, and the accountant of a split walk a
-// light parameter wave. With two split pairs (finders in groups 0 and 1) the heavy roles —
-// accountant 0, finder 0, the helper, accountant 1 — each get a SIMD, next to the light walkers,
-// finder 1 and the task wave. Identity for other block shapes.
-static uint32_t boll_wave_map(int pw, int nsplit, int split_grp, int split_grp2, int xw) {
+// light parameter wave. Identity for other block shapes.
+static uint32_t boll_wave_map(int pw, int nsplit, int xw) {
     uint32_t m = 0;
     for (int w = 0; w < 8; ++w) m |= (uint32_t)w << (4 * w);
     const int nw = pw + 1 + nsplit + xw;
-    if (nw == 8 && pw == 4 && (nsplit < 2 || (split_grp == 0 && split_grp2 == 1))) {
-        // logical roles: 0-3 parameter groups, 4 helper, then the accountants, then tasks
-        const int split2_map[8] = {5, 0, 4, 6, 3, 2, 1, 7};
+    if (nw == 8 && pw == 4) {
+        // logical roles: 0-3 parameter groups, 4 helper, then the accountant, then tasks
         const int split_map[8] = {0, 1, 2, 3, 6, 7, 5, 4};
         const int plain_map[8] = {0, 1, 2, 3, 5, 6, 7, 4};
-        const int* r = nsplit == 2 ? split2_map : (nsplit == 1 ? split_map : plain_map);
+        const int* r = nsplit == 1 ? split_map : plain_map;
         m = 0;
         for (int w = 0; w < 8; ++w) m |= (uint32_t)r[w] << (4 * w);
     }
@@ -1691,8 +1680,8 @@ static int tile_extra_waves(int used, int x) {
 }
 
 size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
-size_t boll_lds_bytes(const Grid& g, int nsplit) {
-    return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd, nsplit).total;
+size_t boll_lds_bytes(const Grid& g) {
+    return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd).total;
 }
 
 int32_t ema_burn_tiles(int32_t max_span) {
@@ -1772,42 +1761,41 @@ hipError_t launch_boll(const SymDesc* syms, int32_t n_sym, const int32_t* high, 
     // the most, and its lanes' serial trade chains set the tile time (config 4: 7.1 walk
     // iterations per tile against 1.0-4.3 for the other waves), so that wave only finds trades
     // and an accountant wave keeps their accounts a tile later.
-    int split_grp = -1, split_grp2 = -1;
+    int split_grp = -1;
     if (tile_split_walk() && pw >= 2 && grid.y == 1) {
         const long long per_k = (long long)g.na * g.nc * g.nd;  // lanes per z threshold
         const int grp = (int)((g.kmin_idx * per_k) / lpw);
         if (grp < pw) split_grp = grp;
     }
-    const int nsplit = split_grp < 0 ? 0 : (split_grp2 < 0 ? 1 : 2);
+    const int nsplit = split_grp < 0 ? 0 : 1;
     const int base = pw + 1 + nsplit;
     // at most one block per CU (config 4 on 8 GPUs: 250 symbols) leaves wave slots free: four
     // task-only waves (8.17 -> 7.90 ms vs two); otherwise as many as keep the block at 8 waves,
-    // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms;
-    // with two split pairs one task wave is left)
+    // so two blocks share a CU at <= 128 VGPRs (config 4: three, 9.65 -> 9.51 ms; four 15.8 ms)
     const bool sparse = (long long)grid.x * grid.y * grid.z <= device_cus();
-    const int xw = tile_extra_waves(base, sparse ? 4 : std::max(nsplit == 2 ? 1 : 2, std::min(3, 8 - base)));
+    const int xw = tile_extra_waves(base, sparse ? 4 : std::max(2, std::min(3, 8 - base)));
     const dim3 block(64 * (base + xw));
-    const size_t lds = boll_lds_bytes(g, nsplit > 0 ? nsplit : 1);
-    const uint32_t wmap = boll_wave_map(pw, nsplit, split_grp, split_grp2, xw);
+    const size_t lds = boll_lds_bytes(g);
+    const uint32_t wmap = boll_wave_map(pw, nsplit, xw);
 #ifdef BT_PROFILING
     if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, true, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
         return hipGetLastError();
     }
 #endif
     if (split) {
         // speculative segments, then the fix pass of each boundary in order (a block returns at
         // once when its lanes' starts were right), then the fold
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
         const dim3 fgrid(grid.x, grid.y, 1);
         for (int s = 1; s < seg.G; ++s)
-            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s, split_grp, split_grp2, wmap);
+            hipLaunchKernelGGL((boll_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, s, split_grp, wmap);
         const size_t n = (size_t)n_sym * g.n_params;
         hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
     } else if (parity) {
-        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<true, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
     } else {
-        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, split_grp2, wmap);
+        hipLaunchKernelGGL((boll_tile_kernel<false, false, false>), grid, block, lds, st, syms, high, low, close, g, out, xw, lpw, seg, 0, split_grp, wmap);
     }
     return hipGetLastError();
 }

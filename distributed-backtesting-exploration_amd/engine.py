@@ -17,11 +17,16 @@ from typing import Sequence
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-# BT_LIB (tuning aid): another in-tree build of the library, e.g. libbt_base.so for an A/B
-LIB_PATH = os.path.join(PKG_DIR, os.path.basename(os.environ.get("BT_LIB", "libbt.so")))
+# BT_LIB (tuning aid): another in-tree build of the library under dev/, e.g. dev/prof.so (the
+# profiling build, `make PROFILING=1`) or dev/base.so for an A/B; nothing outside the package
+_bt_lib = os.path.normpath(os.environ.get("BT_LIB", "libbt.so"))
+if _bt_lib.startswith("..") or os.path.isabs(_bt_lib):
+    raise ImportError(f"BT_LIB={_bt_lib}: a path inside {PKG_DIR} (libbt.so or dev/NAME.so)")
+LIB_PATH = os.path.join(PKG_DIR, _bt_lib)
 CSRC = os.path.join(PKG_DIR, "csrc")
 # include/bt.h BT_ABI_VERSION this wrapper is written against (build() checks the built library)
 ABI_VERSION = 3
+PIPE_SLOTS = 4  # include/bt.h BT_PIPE_SLOTS: pinned read-back / exchange slots
 
 BT_SMA_CROSS, BT_EMA_OLS, BT_BOLL = 1, 2, 3
 BT_FLAG_PARITY, BT_FLAG_TIMING = 1, 2
@@ -161,28 +166,34 @@ def lib():
 
 # Entry points added after ABI version 2 (the multi-GPU exchange), bound on first use: an older
 # library (e.g. a previous round's build, loaded with BT_LIB for a regression check) then still
-# loads and runs everything else.
+# loads and runs everything else. Each carries the first ABI version whose signature it matches:
+# a symbol whose signature changed (bt_exchange_merge gained block_bytes in ABI 3) must not be
+# bound with the new argument list on a library that exports the old one.
 _LATE_SYMBOLS = {
-    "bt_comm_unique_id": ([C.c_void_p], C.c_int32),
-    "bt_comm_create": ([C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_char_p, C.c_size_t],
-                       C.c_void_p),
-    "bt_comm_destroy": ([C.c_void_p], None),
-    "bt_exchange_async": ([C.c_void_p, C.c_void_p, C.c_int32], C.c_int32),
-    "bt_exchange_wait": ([C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p], C.c_int32),
-    "bt_exchange_message_bytes": ([C.c_int32], C.c_int64),
-    "bt_exchange_merge": ([C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
-                           C.c_void_p], C.c_int32),
+    "bt_comm_unique_id": (2, [C.c_void_p], C.c_int32),
+    "bt_comm_create": (2, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                           C.c_size_t], C.c_void_p),
+    "bt_comm_destroy": (2, [C.c_void_p], None),
+    "bt_exchange_async": (2, [C.c_void_p, C.c_void_p, C.c_int32], C.c_int32),
+    "bt_exchange_wait": (2, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p], C.c_int32),
+    "bt_exchange_message_bytes": (2, [C.c_int32], C.c_int64),
+    "bt_exchange_merge": (3, [C.c_void_p, C.c_size_t, C.c_int32, C.c_int32, C.c_void_p, C.c_int32,
+                              C.c_void_p], C.c_int32),
 }
 _late = {}
 
 
 def sym(name: str):
-    """A late (post-v2) entry point of libbt.so, typed on first use; AttributeError if the loaded
-    library predates it."""
+    """A late (post-v2) entry point of libbt.so, typed on first use. BtError if the loaded
+    library's ABI predates the signature bound here (or AttributeError if it lacks the symbol)."""
     f = _late.get(name)
     if f is None:
+        min_abi, argtypes, restype = _LATE_SYMBOLS[name]
+        have = lib().bt_abi_version()
+        if have < min_abi:
+            raise BtError(f"{name}: {LIB_PATH} has ABI {have}, this binding needs ABI >= {min_abi}")
         f = getattr(lib(), name)
-        f.argtypes, f.restype = _LATE_SYMBOLS[name]
+        f.argtypes, f.restype = argtypes, restype
         _late[name] = f
     return f
 
@@ -378,8 +389,9 @@ class Engine:
         return out[:m]
 
     def topk_fetch_async(self, slot: int) -> None:
-        """Enqueue the read-back of the last run's top-k and trade count into pinned slot 0/1
-        (no host wait): the next run can be enqueued before these records are consumed."""
+        """Enqueue the read-back of the last run's top-k and trade count into pinned slot
+        0 .. PIPE_SLOTS-1 (no host wait): later runs can be enqueued before these records are
+        consumed."""
         _check(lib().bt_topk_fetch_async(self._h, slot))
 
     def topk_fetch_wait(self, slot: int, k=None) -> tuple:

@@ -259,11 +259,22 @@ class Worker:
             except queue.Empty:
                 break
         lost = []
+        # one deadline for the whole flush (a hung dispatcher must not block the worker's
+        # shutdown for flush_timeout_s per completion), and after the first deadline or
+        # unavailable error the rest are logged as lost without another attempt
+        deadline = time.monotonic() + self.flush_timeout_s
+        give_up = False
         for jid, data, _, _ in pending:
-            try:  # bounded: a hung dispatcher must not block the worker's shutdown
-                self._complete(P.CompleteRequest(id=jid, data=data), timeout=self.flush_timeout_s)
-            except grpc.RpcError:
+            left = deadline - time.monotonic()
+            if give_up or left <= 0:
                 lost.append(jid)
+                continue
+            try:
+                self._complete(P.CompleteRequest(id=jid, data=data), timeout=left)
+            except grpc.RpcError as why:
+                lost.append(jid)
+                code = why.code() if hasattr(why, "code") else None
+                give_up = code in (grpc.StatusCode.DEADLINE_EXCEEDED, grpc.StatusCode.UNAVAILABLE)
         if lost:
             log.warning("Stopping with %d completions undelivered (the dispatcher re-runs them "
                         "once it prunes this worker): %s", len(lost), ", ".join(lost))

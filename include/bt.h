@@ -188,9 +188,11 @@ int32_t bt_read_sums(bt_engine* e, bt_sums* out, size_t n);             /* parit
 int32_t bt_read_trades(bt_engine* e, bt_trade* out, size_t n);          /* n = sym x param x cap */
 int32_t bt_read_topk(bt_engine* e, bt_topk_rec* out, int32_t k);        /* returns count */
 int32_t bt_read_stats(bt_engine* e, bt_stats* out);
+#define BT_PIPE_SLOTS 4 /* pinned read-back / exchange slots per engine / communicator */
 /* Pipelined read-back of the last run's top-k and trade count: bt_topk_fetch_async enqueues
- * the device-to-host copy into pinned slot 0 or 1 behind the run (no host wait), so the next
- * bt_run can be enqueued before this run's records are consumed; bt_topk_fetch_wait waits for
+ * the device-to-host copy into pinned slot 0 .. BT_PIPE_SLOTS-1 behind the run (no host wait),
+ * so the next bt_run (or the next BT_PIPE_SLOTS - 1) can be enqueued before this run's records
+ * are consumed; bt_topk_fetch_wait waits for
  * that copy only and returns the record count. The device selection is exact on any grid (a
  * tie-heavy one takes a slower single-block finish, k_topk.hip). A slot stays valid until its
  * next fetch. */
@@ -217,8 +219,9 @@ int32_t bt_merge_topk(const bt_topk_rec* in, size_t n, int32_t k, bt_topk_rec* o
  *   rank 0: bt_comm_unique_id(id); the launcher broadcasts the 128 bytes; every rank:
  *   bt_comm_create(id, rank, world, device, k) — a collective call, all ranks together.
  * bt_exchange_async enqueues the exchange of the engine's last run (which needs topk >= k) into
- * pinned slot 0 or 1 behind the run's top-k chain, without a host wait; bt_exchange_wait returns
- * the merged global top-k (count) and counters[2] = {bar-evals, trades} summed over ranks.
+ * pinned slot 0 .. BT_PIPE_SLOTS-1 behind the run's top-k chain, without a host wait;
+ * bt_exchange_wait returns the merged global top-k (count) and counters[2] = {bar-evals, trades}
+ * summed over ranks.
  * Every rank must issue the same sequence of exchanges.
  * RCCL is loaded at run time (dlopen of librccl.so.1 on the first bt_comm_unique_id /
  * bt_comm_create): libbt.so does not link it, so a single-GPU host loads the engine without RCCL,

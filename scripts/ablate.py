@@ -3,7 +3,7 @@ rounds in one process (cdna_hip_programming.md §5.4 rule 24). Outputs are wrong
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
-os.environ.setdefault("BT_LIB", "libbt_prof.so")
+os.environ.setdefault("BT_LIB", "dev/prof.so")
 import dbx_amd as D
 
 S = int(os.environ.get("S", 5000)); BARS = 2520

@@ -3,7 +3,7 @@ meaningless, only the time is read).   [S=symbols] python scripts/ablate_probe.p
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
-os.environ.setdefault("BT_LIB", "libbt_prof.so")
+os.environ.setdefault("BT_LIB", "dev/prof.so")
 cfg = int(sys.argv[1])
 S_OVERRIDE = int(os.environ.get("S", "0"))
 for m in sys.argv[2:]:

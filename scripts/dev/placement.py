@@ -7,7 +7,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-os.environ.setdefault("BT_LIB", "libbt_prof.so")
+os.environ.setdefault("BT_LIB", "dev/prof.so")
 os.environ["BT_ABLATE"] = os.environ.get("BT_ABLATE", "64")
 import dbx_amd as D
 from dbx_amd import engine as E

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Interleaved A/B of in-tree library builds over several shards: R rounds, each running every
 # LIBS entry on every CASES entry ("config:symbols"), printing the kernel average and step time.
-#   LIBS="libbt_base.so libbt.so" CASES="4:500 4:250 3:500 2:5000" R=3 bash scripts/gpu_ab.sh
-# Libraries are built beforehand on the CPU: make -C .../csrc OUT=../libbt_base.so BUILD=../build_base
+#   LIBS="dev/base.so libbt.so" CASES="4:500 4:250 3:500 2:5000" R=3 bash scripts/gpu_ab.sh
+# Libraries are built beforehand on the CPU: make -C .../csrc OUT=../dev/base.so BUILD=../build_base
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/ab
 for r in $(seq ${R:-2}); do
   for lib in ${LIBS:-libbt.so}; do

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of in-tree library builds (LIBS="libbt.so libbt_v1.so ...", built beforehand with
+# A/B of in-tree library builds (LIBS="libbt.so dev/v1.so ...", built beforehand with
 # `make OUT=../libbt_vN.so BUILD=../build_vN EXTRA=-D...`): kernel time of one bench shard each.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/ab
 for lib in ${LIBS:-libbt.so}; do

@@ -2,7 +2,7 @@
 # Launch-variant / knob sweep with the profiling library: each ENVS entry
 # ("NAME=V,NAME2=V2" or "-" for none) timed on the shards SYMS of config CFG (default 4), R
 # interleaved rounds (e.g. ENVS="- BT_ONE_TRIP=1" CFG=2 SYMS=5000; ENVS="BT_LPW=32 BT_XW=3").
-export BT_LIB=${BT_LIB:-libbt_prof.so}
+export BT_LIB=${BT_LIB:-dev/prof.so}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/envs
 for r in $(seq ${R:-2}); do
  for e in ${ENVS:--}; do

@@ -11,7 +11,7 @@ PB="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_V
 for m in ${MASKS:-0 8 2 10}; do
   for p in A B; do
     [ $p = A ] && C="$PA" || C="$PB"
-    BT_LIB=${LIB:-libbt_prof.so} BT_ABLATE=$m timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d $O/m$m$p -o sq -- python3 bench.py --config ${CFG:-4} --symbols ${SYMS:-500} --steps 3 --warmup 1 --no-cpu-baseline --topk 0 > $O/m$m$p.log 2>&1 || { tail -5 $O/m$m$p.log; exit 1; }
+    BT_LIB=${LIB:-dev/prof.so} BT_ABLATE=$m timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d $O/m$m$p -o sq -- python3 bench.py --config ${CFG:-4} --symbols ${SYMS:-500} --steps 3 --warmup 1 --no-cpu-baseline --topk 0 > $O/m$m$p.log 2>&1 || { tail -5 $O/m$m$p.log; exit 1; }
   done
   python3 - "$O/m$m" "$m" <<'PY'
 import csv, glob, collections, json, sys

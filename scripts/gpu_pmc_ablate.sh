@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the config-2 SMA kernel with phases removed (BT_ABLATE masks; outputs wrong by
 # design): where the VALU / LDS instructions and LDS cycles go. One counter group per run.
-export BT_LIB=${BT_LIB:-libbt_prof.so}  # profiling build (make PROFILING=1)
+export BT_LIB=${BT_LIB:-dev/prof.so}  # profiling build (make PROFILING=1)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/pmca
 export TMPDIR=/tmp
 for m in ${MASKS:-0 1 2 4 8 12 15}; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ instruction counters of the config-4 Bollinger kernel (500 symbols) with phases removed
 # (profiling build, BT_ABLATE masks: 8 no walks, 2 no flag tasks; outputs wrong by design).
-export BT_LIB=${BT_LIB:-libbt_prof.so}
+export BT_LIB=${BT_LIB:-dev/prof.so}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/pmc4a
 export TMPDIR=/tmp
 C="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS"

@@ -10,4 +10,4 @@ for G in 4 5 6 8; do
   timeout -k 10 200 python3 bench.py --config 5 --symbols 1250 --segments $G --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r04/c5_G$G.log 2>&1 || { tail -5 gpurun_out/r04/c5_G$G.log; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/r04/c5_G$G.log').read().strip().splitlines()[-1]); print('config 5 1250 G', $G, 'kernel', round(d['roofline']['kernel_avg_ms'],3))"
 done
-LIBS="libbt_base.so libbt.so libbt_base.so libbt.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1
+LIBS="dev/base.so libbt.so dev/base.so libbt.so" CFG=5 SYMS="1250" bash scripts/gpu_ab_libs.sh || exit 1

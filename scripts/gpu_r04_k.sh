@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4: one |z| > k word per (window, k), split by the sign of D in the walk (libbt_v6.so) vs HEAD (libbt_h5.so).
+# Round 4: one |z| > k word per (window, k), split by the sign of D in the walk (dev/v6.so) vs HEAD (dev/h5.so).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r04
 export PYTHONUNBUFFERED=1
-LIBS="libbt_h5.so libbt_v6.so libbt_h5.so libbt_v6.so" CFG=4 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
+LIBS="dev/h5.so dev/v6.so dev/h5.so dev/v6.so" CFG=4 SYMS="500 250" bash scripts/gpu_ab_libs.sh || exit 1
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-BT_LIB=libbt_v6.so timeout -k 10 900 $T tests -m gpu > gpurun_out/r04/pytest_k.log 2>&1 || { tail -30 gpurun_out/r04/pytest_k.log; exit 1; }
+BT_LIB=dev/v6.so timeout -k 10 900 $T tests -m gpu > gpurun_out/r04/pytest_k.log 2>&1 || { tail -30 gpurun_out/r04/pytest_k.log; exit 1; }
 tail -1 gpurun_out/r04/pytest_k.log

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r04
 export PYTHONUNBUFFERED=1
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-BT_LIB=libbt_pre.so timeout -k 10 300 $T tests/test_gpu_narrow.py -m gpu -k level_fills > gpurun_out/r04/narrow_pre.log 2>&1
+BT_LIB=dev/pre.so timeout -k 10 300 $T tests/test_gpu_narrow.py -m gpu -k level_fills > gpurun_out/r04/narrow_pre.log 2>&1
 rc=$?; echo "pre-fix library: rc=$rc (1 = the test caught the overflow)"; tail -3 gpurun_out/r04/narrow_pre.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 600 $T tests -m gpu > gpurun_out/r04/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/r04/pytest_gpu.log; exit 1; }

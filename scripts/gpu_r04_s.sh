@@ -2,7 +2,7 @@
 # Round 4: Bollinger hardware-wave role maps (profiling build, BT_WAVEMAP) on config 4's shards:
 # the default (accountant beside parameter wave 2) and three others, twice each.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/wm
-export BT_LIB=libbt_prof.so
+export BT_LIB=dev/prof.so
 for rep in 1 2; do
 for m in 45763210 45763120 54763210 47563210; do
   for s in 500 250; do

@@ -2,7 +2,7 @@
 # Round 4: config 3 wave priorities (profiling build; BT_ABLATE bit 20 + 2-bit fields: chain at
 # bit 16, walk at 18, helper A's scan at 22): the default (0, 2, 0) against a raised scan.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/prio3
-export BT_LIB=libbt_prof.so
+export BT_LIB=dev/prof.so
 for rep in 1 2; do
 for m in 1572864 5767168 9961472 14155776 5832704 10027008; do
   for s in 500 250; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: config 4 task-only waves per block (profiling build, BT_XW): 1 vs the default 2.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/xw
-export BT_LIB=libbt_prof.so
+export BT_LIB=dev/prof.so
 for rep in 1 2; do
 for xw in 2 1; do
   for s in 500 250; do

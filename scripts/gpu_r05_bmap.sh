@@ -7,7 +7,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 for rep in 1 2; do
   for m in 45763210 54763210 63475210 34762150; do
     for s in 500 250; do
-      BT_LIB=libbt_prof.so BT_WAVEMAP=$m timeout -k 10 200 python3 bench.py --config 4 --symbols $s --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r05/bmap/b_${m}_$s.log 2>&1 || { tail -5 gpurun_out/r05/bmap/b_${m}_$s.log; exit 1; }
+      BT_LIB=dev/prof.so BT_WAVEMAP=$m timeout -k 10 200 python3 bench.py --config 4 --symbols $s --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r05/bmap/b_${m}_$s.log 2>&1 || { tail -5 gpurun_out/r05/bmap/b_${m}_$s.log; exit 1; }
       python3 -c "import json; d=json.loads(open('gpurun_out/r05/bmap/b_${m}_$s.log').read().strip().splitlines()[-1]); print('map', '$m', 'config 4', $s, 'kernel', round(d['roofline']['kernel_avg_ms'],3))"
     done
   done

@@ -2,7 +2,7 @@
 # Round 5: the trade-parallel Bollinger kernel, timing (HEAD vs the round-4 kernel) and stamps.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r05
 export PYTHONUNBUFFERED=1
-for lib in libbt.so libbt_r4.so; do
+for lib in libbt.so dev/r4.so; do
   for s in 500 250; do
     BT_LIB=$lib timeout -k 10 200 python3 bench.py --config 4 --symbols $s --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r05/c4_${lib}_$s.log 2>&1 || { tail -5 gpurun_out/r05/c4_${lib}_$s.log; exit 1; }
     python3 -c "import json; d=json.loads(open('gpurun_out/r05/c4_${lib}_$s.log').read().strip().splitlines()[-1]); print('$lib config 4', $s, 'kernel', round(d['roofline']['kernel_avg_ms'],3), 'ms/step', round(d['ms_per_step'],3))"

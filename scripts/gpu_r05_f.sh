@@ -6,7 +6,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 timeout -k 10 400 $T tests/test_gpu_segments.py tests/test_gpu_fullsize.py -m gpu -k "sma or config5 or random" > gpurun_out/r05/c5/seg_tests.log 2>&1 || { tail -30 gpurun_out/r05/c5/seg_tests.log; exit 1; }
 tail -1 gpurun_out/r05/c5/seg_tests.log
-for lib in libbt.so libbt_r4.so; do
+for lib in libbt.so dev/r4.so; do
 
   BT_LIB=$lib WORLD_SIZE=1 timeout -k 10 300 python3 bench.py --config 5 --symbols 1250 --scaling strong --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/r05/c5/b_$lib.log 2>&1 || { tail -5 gpurun_out/r05/c5/b_$lib.log; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/r05/c5/b_$lib.log').read().strip().splitlines()[-1]); print('$lib config 5 shard kernel', round(d['roofline']['kernel_avg_ms'],2), 'ms/step', round(d['ms_per_step'],2), d['bar_segments'])"
@@ -16,7 +16,7 @@ for lib in libbt.so libbt_r4.so; do
 done
 python3 - <<'PY'
 import csv, glob, collections
-for lib in ("libbt.so", "libbt_r4.so"):
+for lib in ("libbt.so", "dev/r4.so"):
     tot = {}
     for pass_ in ("FETCH_SIZE", "WRITE_SIZE"):
         f = glob.glob(f"gpurun_out/r05/c5/{lib}_{pass_}/**/*counter_collection.csv", recursive=True)

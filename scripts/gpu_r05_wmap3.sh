@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/r05/wmap
 for rep in 1 2; do
 for m in 76543210 76524310 76524301 76514320; do
   for s in 500 250; do
-    BT_LIB=libbt_prof.so BT_EMA_WAVEMAP=$m timeout -k 10 200 python3 bench.py --config 3 --symbols $s --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r05/wmap/c3_${m}_$s.log 2>&1 || { tail -5 gpurun_out/r05/wmap/c3_${m}_$s.log; exit 1; }
+    BT_LIB=dev/prof.so BT_EMA_WAVEMAP=$m timeout -k 10 200 python3 bench.py --config 3 --symbols $s --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/r05/wmap/c3_${m}_$s.log 2>&1 || { tail -5 gpurun_out/r05/wmap/c3_${m}_$s.log; exit 1; }
     python3 -c "import json; d=json.loads(open('gpurun_out/r05/wmap/c3_${m}_$s.log').read().strip().splitlines()[-1]); print('map $m config 3 $s kernel', round(d['roofline']['kernel_avg_ms'],3))"
   done
 done

@@ -8,7 +8,7 @@ for r in $(seq ${R:-2}); do
   for c in ${CASES}; do
     IFS=: read cfg s g xw <<< "$c"
     if [ "$xw" = "-" ]; then unset BT_XW; else export BT_XW=$xw; fi
-    BT_LIB=${LIB:-libbt_prof.so} timeout -k 10 200 python3 bench.py --config $cfg --symbols $s --segments $g --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/shape/b.log 2>&1 || { tail -5 gpurun_out/shape/b.log; exit 1; }
+    BT_LIB=${LIB:-dev/prof.so} timeout -k 10 200 python3 bench.py --config $cfg --symbols $s --segments $g --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/shape/b.log 2>&1 || { tail -5 gpurun_out/shape/b.log; exit 1; }
     python3 -c "import json; d=json.loads(open('gpurun_out/shape/b.log').read().strip().splitlines()[-1]); print('round $r', 'config $cfg symbols $s segments $g xw $xw', 'kernel', round(d['roofline']['kernel_avg_ms'],4), 'ms/step', round(d['ms_per_step'],4), d.get('bar_segments'))"
   done
 done

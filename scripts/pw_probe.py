@@ -4,7 +4,7 @@
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
-os.environ.setdefault("BT_LIB", "libbt_prof.so")
+os.environ.setdefault("BT_LIB", "dev/prof.so")
 import dbx_amd as D
 cases = [(4, 250, (4, 2, 1)), (4, 500, (4, 2)), (3, 250, (1,)), (3, 500, (1,))]
 for cfg, S, pws in cases:

@@ -3,7 +3,7 @@ BT_ABLATE=64). Shares only — stamps perturb the schedule (cdna_hip_programming
 import ctypes as C, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # ablation / stamps / launch overrides exist only in the profiling build (make PROFILING=1)
-os.environ.setdefault("BT_LIB", "libbt_prof.so")
+os.environ.setdefault("BT_LIB", "dev/prof.so")
 os.environ["BT_ABLATE"] = os.environ.get("BT_ABLATE", "64")
 import dbx_amd as D
 from dbx_amd import engine as E

@@ -59,6 +59,19 @@ def test_abi_version_and_no_gpu_failure():
         D.Engine(D.Grid.sma([600, 4096], [4096, 4000]))
 
 
+def test_late_symbols_check_the_library_abi(monkeypatch):
+    # every late entry point binds on the current library ...
+    for name in E._LATE_SYMBOLS:
+        assert E.sym(name) is not None
+    # ... and a library older than a symbol's signature is refused, not bound with shifted
+    # arguments (bt_exchange_merge gained block_bytes in ABI 3)
+    monkeypatch.setattr(E, "_late", {})
+    min_abi, args, res = E._LATE_SYMBOLS["bt_exchange_merge"]
+    monkeypatch.setitem(E._LATE_SYMBOLS, "bt_exchange_merge", (D.ABI_VERSION + 1, args, res))
+    with pytest.raises(D.BtError, match="needs ABI"):
+        E.sym("bt_exchange_merge")
+
+
 def test_config_validation():
     with pytest.raises(D.BtError, match="empty axis"):
         D.Engine(D.Grid.sma([], [10]))
@@ -121,7 +134,7 @@ def test_merge_topk_order():
 
 def test_release_library_reads_no_environment():
     """The release libbt.so has no profiling switches: phase ablation (BT_ABLATE), s_memtime
-    stamps and launch overrides exist only in libbt_prof.so (`make PROFILING=1`), so no stray
+    stamps and launch overrides exist only in dev/prof.so (`make PROFILING=1`), so no stray
     environment variable in a worker can change a backtest result."""
     blob = open(E.LIB_PATH, "rb").read()
     for name in (b"BT_ABLATE", b"BT_PW", b"BT_XW", b"BT_LPW", b"BT_ONE_TRIP"):

@@ -56,7 +56,12 @@ def test_torchrun_two_ranks_exchange_equals_single_engine(config, extra):
     # per-rank attribution of a scaling loss
     pr = d["per_rank"]
     assert len(pr["kernel_avg_ms"]["by_rank"]) == 2 and pr["kernel_avg_ms"]["min"] > 0
-    assert len(pr["exchange_wait_ms_per_step"]["by_rank"]) == 2
+    assert len(pr["host_wait_ms_per_step"]["by_rank"]) == 2
+    # two steps in flight at N > 1; the gloo exchange proper is timed apart from the GPU wait
+    #  and is a small share of the step
+    assert pr["pipeline_depth"] == 2 and pr["ranks_share_device"]
+    step_ms = d["ms_per_step"]
+    assert 0 <= pr["exchange_ms_per_step"]["max"] < step_ms
     assert sum(pr["symbols"]) == d["config"]["symbols_total"]
     assert "gloo all-gather" in d["config"]["parallelism"], d["config"]["parallelism"]
     v = d["verified_exchange"]

@@ -360,28 +360,37 @@ def test_spec_maximum_windows(strategy):
 
 
 def test_pipelined_topk_fetch():
-    """bench.py's pipelining: run i+1 is enqueued before run i's top-k is read; each slot must
-    hold its own run's records and trade count (same as the synchronous read of that run).
-    Reloading the data between the runs must not race the previous run's top-k chain, which
-    reads the symbol descriptors on the second stream (round 2: a reload overwrote them first
-    and slot 0 reported symbol 305 for 5); repeated, since a race shows only sometimes."""
+    """bench.py's pipelining: runs i+1 .. i+depth are enqueued before run i's top-k is read;
+    each slot must hold its own run's records and trade count (same as the synchronous read of
+    that run), with every slot in flight at once (runs i and i+2 share a summary buffer, which
+    the engine orders behind run i's read-back). Reloading the data between the runs must not
+    race the previous run's top-k chain, which reads the symbol descriptors on the second
+    stream (round 2: a reload overwrote them first and slot 0 reported symbol 305 for 5);
+    repeated, since a race shows only sometimes."""
     grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
+    firsts = [300 * i for i in range(D.PIPE_SLOTS)]
     with D.Engine(grid, topk=20) as e:
         refs = []
-        for first in (0, 300):
+        for first in firsts:
             e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
             e.run()
             refs.append((e.read_topk(), e.stats()["trades"]))
-        for _ in range(6):
-            e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
-            e.run()
-            e.topk_fetch_async(0)
-            e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)   # drains the top-k chain of slot 0 first
-            e.run()
-            e.topk_fetch_async(1)
+        for _ in range(4):
+            for slot, first in enumerate(firsts):
+                e.load_synthetic(9, first, 40, 700, D.BT_DAILY)  # drains the earlier top-k chains
+                e.run()
+                e.topk_fetch_async(slot)
             for slot, (top, trades) in enumerate(refs):
                 got, n = e.topk_fetch_wait(slot)
                 assert got.tolist() == top.tolist() and n == trades
+        # the same data, no reload: PIPE_SLOTS runs back to back, as bench.py issues them
+        e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
+        for slot in range(D.PIPE_SLOTS):
+            e.run()
+            e.topk_fetch_async(slot)
+        for slot in range(D.PIPE_SLOTS):
+            got, n = e.topk_fetch_wait(slot)
+            assert got.tolist() == refs[0][0].tolist() and n == refs[0][1]
 
 
 @pytest.mark.parametrize("hi_prices", [False, True])
@@ -410,7 +419,7 @@ def test_sma_large_window_products(hi_prices):
 
 
 def test_release_library_ignores_ablate_env(monkeypatch):
-    """BT_ABLATE in the environment (a profiling switch of libbt_prof.so) must not change a
+    """BT_ABLATE in the environment (a profiling switch of dev/prof.so) must not change a
     release-library result: bit-identical summaries with and without it."""
     grid = D.Grid.boll([10, 45], [3, 5], [50], [100, 400], k_den=2)
     res = []
@@ -549,27 +558,29 @@ def test_run_batch_binary_and_csv_mixed():
 
 def test_rccl_exchange_world1_matches_local_topk():
     """The C-ABI RCCL exchange (bt_comm_*, comm.cpp) at world size 1 on the MI355X: an
-    all-gather from the engine's device top-k, pipelined over both slots, returns that run's
-    top-k and counters exactly."""
+    all-gather from the engine's device top-k, pipelined over every slot (BT_PIPE_SLOTS runs in
+    flight before the first wait, as bench.py's two-deep N > 1 loop needs three), returns each
+    run's top-k and counters exactly."""
     grid = D.Grid.sma([4, 6, 10], [50, 60, 120], annualization=252)
     comm = E.Comm(E.Comm.unique_id(), 0, 1, 0, 20)
+    firsts = [300 * i for i in range(D.PIPE_SLOTS)]
     try:
         with D.Engine(grid, topk=20) as e:
             refs = []
-            for first in (0, 300):
+            for first in firsts:
                 e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
                 e.run()
                 refs.append((e.read_topk(), e.stats()))
-            e.load_synthetic(9, 0, 40, 700, D.BT_DAILY)
-            e.run()
-            comm.exchange_async(e, 0)
-            e.load_synthetic(9, 300, 40, 700, D.BT_DAILY)
-            e.run()
-            comm.exchange_async(e, 1)
+            for slot, first in enumerate(firsts):
+                e.load_synthetic(9, first, 40, 700, D.BT_DAILY)
+                e.run()
+                comm.exchange_async(e, slot)
             for slot, (top, st) in enumerate(refs):
                 got, cnt = comm.exchange_wait(slot)
                 assert got.tolist() == top.tolist()
                 assert cnt == [st["bar_evals"], st["trades"]]
+            with pytest.raises(D.BtError, match="bad arguments"):
+                comm.exchange_async(e, D.PIPE_SLOTS)
     finally:
         comm.close()
 

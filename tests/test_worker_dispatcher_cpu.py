@@ -203,8 +203,37 @@ def test_pending_retries_get_a_last_attempt_and_a_log_on_stop(caplog):
         with caplog.at_level(logging.WARNING):
             w._flush_retries()
         assert sent == ["j1"] and not w._retry
-        assert timeouts == [w.flush_timeout_s] * 3 and w.flush_timeout_s > 0
+        # one deadline for the whole flush: every attempt gets what is left of it
+        assert len(timeouts) == 3 and w.flush_timeout_s > 0
+        assert all(0 < t <= w.flush_timeout_s for t in timeouts) and timeouts == sorted(timeouts, reverse=True)
         assert "2 completions undelivered" in caplog.text and "j2" in caplog.text and "j3" in caplog.text
+    finally:
+        w.channel.close()
+
+
+def test_flush_stops_at_the_first_deadline(caplog):
+    """a hung dispatcher costs the shutdown one deadline, not one per completion:
+    after DEADLINE_EXCEEDED the remaining completions are logged as lost without an attempt."""
+    import grpc
+    import logging
+
+    class Hung(grpc.RpcError):
+        def code(self):
+            return grpc.StatusCode.DEADLINE_EXCEEDED
+    calls = []
+
+    def hung(req, timeout=None):
+        calls.append(req.id)
+        raise Hung()
+    w = WK.Worker("127.0.0.1:1", lambda jobs: ["ok"] * len(jobs), cores=1)
+    w._complete = hung
+    try:
+        for i in range(5):
+            w.complete_q.put((f"j{i}", "ok"))
+        with caplog.at_level(logging.WARNING):
+            w._flush_retries()
+        assert calls == ["j0"]
+        assert "5 completions undelivered" in caplog.text and "j4" in caplog.text
     finally:
         w.channel.close()
 
