@@ -141,7 +141,9 @@ int32_t sma_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
                           int32_t burn_tiles);
 constexpr int kSmaBurnTiles = 2;
 int device_cus();  // compute units of the current device
-size_t ema_lds_bytes(const Grid& g);   // dynamic LDS of the EMA+OLS tile kernel
+// dynamic LDS of the EMA+OLS tile kernel with ts tiles per stage, and the ts an unsplit launch uses
+size_t ema_lds_bytes(const Grid& g, int ts);
+int ema_stage_tiles(const Grid& g);
 size_t boll_lds_bytes(const Grid& g);  // dynamic LDS of the Bollinger tile kernel
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, const SegArgs& seg, hipStream_t st);

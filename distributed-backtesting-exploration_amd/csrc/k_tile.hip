@@ -55,6 +55,30 @@ constexpr int kEStride = kTile + 1;  // ema buffer row stride (doubles): conflic
 // Bollinger tile buffers: scanned (k+2), flagged (k+1), walked (k) and accounted (k-1, by the
 // accountant wave of a split walk)
 constexpr int kBollStages = 4;
+// EMA+OLS runs stages of TS tiles per barrier (ema_tile_kernel): closes, returns and narrow
+// flags of three stages in flight (scanned st+2, flagged st+1, walked st), drawdown tables, chain
+// values and condition words of two (built / chained / flagged st+1 or st+2, read a stage later)
+__host__ __device__ constexpr int ema_ct_slots(int ts) { return 3 * ts; }
+__host__ __device__ constexpr int ema_slots(int ts) { return 2 * ts; }
+// drawdown tables: 64-bar stages build them in the scan (three stages of buffers, as the closes),
+// 128-bar stages a stage later (two)
+__host__ __device__ constexpr int ema_dst_slots(int ts) { return ts == 1 ? ema_ct_slots(1) : ema_slots(ts); }
+// 128-bar stages (TS = 2) for unsplit runs; bar segments (SEG) keep 64-bar stages
+#ifndef BT_EMA_SEG_TS
+#define BT_EMA_SEG_TS 1
+#endif
+constexpr int kEmaTS = 2, kEmaSegTS = BT_EMA_SEG_TS;
+// with 128-bar stages the drawdown tables of a stage are the first tasks of the round that flags
+// it (helper A, which scans, then has only the scans): config 3 task waves were idle ~2.5k
+// cycles per tile while helper A paced at ~3.9k
+#ifndef BT_EMA_DST_TASK
+#define BT_EMA_DST_TASK 1
+#endif
+constexpr bool kEmaDstTask = BT_EMA_DST_TASK;
+#ifndef BT_EMA_CHAIN_TASKS
+#define BT_EMA_CHAIN_TASKS 0
+#endif
+constexpr bool kEmaChainTasks = BT_EMA_CHAIN_TASKS;
 // Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
 // after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
 constexpr int kRecCap = 33;
@@ -83,18 +107,21 @@ struct TileLds {
     size_t r1, r2, ct, ql, dst, stl, sth, ebuf, words, win, lev, levp, levf, lvb, rec, nrec, nar, ctr, total;
 };
 
-// kind 0 = EMA+OLS (na spans, nb windows), 1 = Bollinger (na windows, nb ks, nlev SL/TP levels
-// per side: nsl + ntp)
-__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0) {
+// kind 0 = EMA+OLS (na spans, nb windows, ts tiles per stage), 1 = Bollinger (na windows, nb ks,
+// nlev SL/TP levels per side: nsl + ntp)
+__host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, int nb, int nlev = 0,
+                                                  int ts = kEmaTS) {
     TileLds L{};
     size_t o = 0;
     auto take = [&](size_t bytes) { size_t r = o; o += (bytes + 15) & ~size_t(15); return r; };
-    const int ns = kind == 1 ? kBollStages : kTileStages;
+    // tile buffers: Bollinger kBollStages (one per 64-bar pipeline stage); EMA ema_ct_slots
+    // for closes / returns / narrow flags and ema_slots for tables, chain values and words
+    const int ns = kind == 1 ? kBollStages : ema_ct_slots(ts), nd = kind == 1 ? kBollStages : ema_dst_slots(ts);
     L.r1 = take((size_t)ring * 8);
     L.r2 = take((size_t)ring * (kind == 0 ? 8 : 16));
     L.ct = take((size_t)ns * kTile * 4);
     L.ql = take((size_t)ns * 2 * kTile * 8);
-    L.dst = take((size_t)ns * kDstLevels * kTile * sizeof(Agg));
+    L.dst = take((size_t)nd * kDstLevels * kTile * sizeof(Agg));
     if (kind == 1) {
         L.stl = take((size_t)ns * kLH * 4);  // lows, highs, block and in-block suffix extrema
         L.ebuf = take((size_t)nb * 8);                              // k_num^2 as doubles
@@ -109,8 +136,8 @@ __host__ __device__ inline TileLds tile_lds_layout(int kind, int ring, int na, i
         L.nrec = take((size_t)2 * kTile);
         L.nar = take((size_t)ns * 4);  // per tile stage: the accountant's sums fit int32 (Acct32)
     } else {
-        L.ebuf = take((size_t)2 * na * kEStride * 8);
-        L.words = take((size_t)2 * (4 * na + 2 * nb) * 8);
+        L.ebuf = take((size_t)ema_slots(ts) * na * kEStride * 8);
+        L.words = take((size_t)ema_slots(ts) * (4 * na + 2 * nb) * 8);
         L.win = take((size_t)nb * 4);
         L.nar = take((size_t)ns * 4);  // per tile stage: the walk's accounts fit int32 (Acct32)
     }
@@ -282,14 +309,19 @@ __device__ __forceinline__ void stamp_place(unsigned long long* dbg, int hw_wave
 // starts meet bit for bit once the start's error has decayed below rounding (from the estimate:
 // <= 4 spans of bars; from e = c: ~16), after which they are identical. The fix pass compares
 // them too and re-walks from the true values.
-template <bool PARITY, bool STAMPS, bool SEG>
+template <bool PARITY, bool STAMPS, bool SEG, int TS>
 __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restrict__ syms,
                                                         const int32_t* __restrict__ close,
                                                         Grid g, Out out, int nextra, int lpw,
                                                         SegArgs sg, int fix_seg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nsp = g.na, nol = g.nb, R = g.ring;
-    const TileLds LL = tile_lds_layout(0, R, nsp, nol);
+    const TileLds LL = tile_lds_layout(0, R, nsp, nol, 0, TS);
+    static_assert(TS == 1 || TS == 2, "64- or 128-bar stages");
+    constexpr int CT = ema_ct_slots(TS), SL = ema_slots(TS), DS = ema_dst_slots(TS);
+    // drawdown tables: built by the scan from its registers (64-bar stages), as the first tasks
+    // of the round that flags their stage (DSTT), or by helper A a stage after the scan
+    constexpr bool DSCAN = TS == 1, DSTT = kEmaDstTask && TS == 2;
     uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);  // sum_{i<x} c_i
     uint64_t* r2 = reinterpret_cast<uint64_t*>(smem + LL.r2);  // sum_{i<x} i*c_i (mod 2^64)
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
@@ -314,7 +346,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int i_n = pj / nol, i_w = pj % nol;
     const int warm = max(g.a[i_n], g.b[i_w]) - 1;
     const int32_t* crow = close + sd.off;
-    const int nword = 4 * nsp + 2 * nol, ntask = max(nsp, nol);
+    // tasks per stage: the drawdown tables of its tiles (DSTT), then one per span / OLS window
+    const int nword = 4 * nsp + 2 * nol, ntask = max(nsp, nol) + (DSTT ? TS : 0);
     const int estage = nsp * kEStride;
 
     SegRange sr{0, 0, 0, 0, ntiles};
@@ -403,9 +436,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         // prefix entry x (sum over scanned bars < x) sits at x mod R: the scan's base is 0
         r1[(T_scan * kTile) % R] = 0;
         r2[(T_scan * kTile) % R] = 0;
-        // task rounds are numbered by tile (flags): the counter starts at round T_scan
-        const int ngrab0 = nwaves - (nextra >= 2 ? npw : 0);
-        *ctr = (uint32_t)T_scan * (uint32_t)(ntask + ngrab0);
+        // task rounds are numbered by stage (flags), from 0
+        *ctr = 0;
     }
     double alpha = 0.0, ema = 0.0, ema_start = 0.0;
     if (helperB && lane < nsp) {
@@ -424,18 +456,36 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 
     TileCarry cy{0, (T_scan > 0 && T_scan * kTile - 1 < B) ? crow[T_scan * kTile - 1] : 0};
     uint64_t cy2 = 0;
-    int32_t cpre = 0;
 
+    // Stages of TS tiles (TS = 2: 128 bars per barrier): stage st holds tiles T_scan + TS st ..
+    // T_scan + TS st + TS - 1 (those past T_end absent). Per stage, one barrier:
+    //   helper A: scans stage st + 2 (closes, returns, prefix rings) and, unless the tables are
+    //             tasks (DSTT), builds the drawdown tables of stage st + 1 from its staged closes (a
+    //             stage after the scan, so the tables need two stages of buffers, not three: 80 KB
+    //             per block at TS = 2);
+    //   helper B: chains stage st + 2;
+    //   the other waves: the tasks of stage st + 1 (DSTT: its tables, then one task per span /
+    //             window over all its tiles);
+    //   parameter waves: walk stage st, tile by tile.
+    // Buffers by tile T: closes, returns, narrow flags T % CT (written st + 2, read st + 1 and st);
+    // tables, chain values, words T % SL.
+    const int nstage = (T_end - T_scan + TS - 1) / TS;
     auto scan = [&](int T, int32_t c) {
-        const int s = T % kTileStages, t0 = T * kTile, t = t0 + lane;
+        const int s = T % CT, t0 = T * kTile, t = t0 + lane;
         const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
-                                      dst + s * kDstLevels * kTile, cy, !BT_ABL(g, 512),
+                                      dst + (T % DS) * kDstLevels * kTile, cy, DSCAN && !BT_ABL(g, 512),
                                       (SEG || !kEmaNarrow) ? nullptr : nars + s);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (uint64_t)pre;
         const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end
         r2[pt] = cy2 + (uint64_t)inc2;
         cy2 += (uint64_t)lane63_i64(inc2);
+    };
+    // drawdown sparse table of tile T from its staged closes (lane = bar; 0 past the end, as the
+    // scan saw them)
+    auto dbuild = [&](int T) {
+        if (BT_ABL(g, 512)) return;  // (profiling ablation: no table)
+        dst_build(cts[(T % CT) * kTile + lane], lane, dst + (T % DS) * kDstLevels * kTile);
     };
 
     // EMA chains of tile T, lane = span, from the tile's closes cl (lane = bar) that helper B
@@ -444,7 +494,7 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     auto chain = [&](int T, int32_t cl) {
         if (SEG && T < chain_T0) return;  // fix pass: bars before the segment are not needed
         const int t1 = T * kTile;
-        double* E = ebuf + (T & 1) * estage + lane * kEStride;
+        double* E = ebuf + (T % SL) * estage + lane * kEStride;
         // three dependent fp64 operations per bar; raising its priority over the walk no longer
         // pays (the walk, tasks, scan and chain all set the tile together: DESIGN.md §4.2)
         if (!BT_ABL(g, 32)) set_prio(BT_PRIO(g, 16, kEmaChainPrio));
@@ -452,8 +502,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         // then one broadcast LDS read issued ahead of the chain instead of a readlane and a
         // conversion on it; span 0 overwrites bar b only after every span has read it (one
         // wave, LDS in program order)
-        const double* CD = ebuf + (T & 1) * estage;
-        if (nsp > 0) ebuf[(T & 1) * estage + lane] = (double)cl;
+        const double* CD = ebuf + (T % SL) * estage;
+        if (nsp > 0) ebuf[(T % SL) * estage + lane] = (double)cl;
         if (lane < nsp && !BT_ABL(g, 256)) {  // profiling: 256 drops the chain, 128 its math
             if (BT_ABL(g, 128)) {
 #pragma unroll
@@ -498,78 +548,124 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     // with task-only waves present the parameter waves only walk: the walk is the per-tile
     // critical path (config 3: ~3.7k of ~4.9k cycles per tile on the parameter wave)
     const bool walk_only = nextra >= 2;
-    const bool no_tasks = walk_only && wave < npw;
-    const int ngrab = nwaves - (walk_only ? npw : 0);
+    // ... and helper B (the chain, which sets the stage with task waves idle) takes none either:
+    // its grab after the chain would only find the round empty
+    const bool chain_only = walk_only && !kEmaChainTasks;
+    const bool no_tasks = (walk_only && wave < npw) || (chain_only && helperB);
+    const int ngrab = nwaves - (walk_only ? npw : 0) - (chain_only ? 1 : 0);
 
-    // condition words of tile T, tasks grabbed dynamically (round T), lane = bar. Task o pairs
-    // span o with OLS window o (either may be absent): both rows' LDS reads are issued together,
-    // and the window length comes from a register (winreg, lane = window), so a task costs one
-    // dependent LDS round trip after its grab.
-    auto flags = [&](int T) {
+    // condition words of stage st (its TS tiles), tasks grabbed dynamically (round st), lane =
+    // bar. Task o pairs span o with OLS window o (either may be absent) over every tile of the
+    // stage: all LDS reads of the task are issued together, and the window length comes from a
+    // register (winreg, lane = window), so a task costs one dependent LDS round trip after its
+    // grab. A stage's tiles past T_end are computed on stale rows and not stored.
+    auto flags = [&](int st) {
         if (no_tasks) return;
-        const int s = T % kTileStages, t = T * kTile + lane;
-        const int32_t cl = cts[s * kTile + lane];
-        const double cd = (double)cl, lhs = cd * 10000.0;
-        uint64_t* Wd = words + (T & 1) * nword;
-        const double* E = ebuf + (T & 1) * estage;
-        const int ptop = ring_pos(T, lane, R);
-        const uint64_t P1t = r1[ptop], P2t = r2[ptop];
-        const uint64_t tin = ballot(t < B);  // bars of the tile inside the series
-        const uint32_t base = (uint32_t)T * (uint32_t)(ntask + ngrab);
+        const int T0 = T_scan + TS * st;
+        const int nt = min(TS, T_end - T0);  // tiles of the stage (wave-uniform)
+        double cd[TS], lhs[TS];
+        uint64_t* Wd[TS];
+        const double* Er[TS];
+        int pt[TS];
+        uint64_t P1[TS], P2[TS], tin[TS];
+#pragma unroll
+        for (int u = 0; u < TS; ++u) {
+            const int T = T0 + u, t = T * kTile + lane;
+            cd[u] = (double)cts[(T % CT) * kTile + lane];
+            lhs[u] = cd[u] * 10000.0;
+            Wd[u] = words + (T % SL) * nword;
+            Er[u] = ebuf + (T % SL) * estage;
+            pt[u] = ring_pos(T, lane, R);
+            P1[u] = r1[pt[u]];
+            P2[u] = r2[pt[u]];
+            tin[u] = ballot(t < B);  // bars of the tile inside the series
+        }
+        const uint32_t base = (uint32_t)st * (uint32_t)(ntask + ngrab);
         uint32_t o = grab_value(grab_issue(ctr, lane)) - base;
+        if (DSTT) {  // the round's first TS tasks: the tiles' drawdown tables
 #pragma unroll 1
-        while (o < (uint32_t)ntask) {
+            while (o < (uint32_t)TS) {
+                const uint32_t vn = grab_issue(ctr, lane);
+                if ((int)o < nt) dbuild(T0 + (int)o);
+                o = grab_value(vn) - base;
+            }
+            o -= TS;
+        }
+#pragma unroll 1
+        while (o < (uint32_t)(ntask - (DSTT ? TS : 0))) {
             const uint32_t vn = grab_issue(ctr, lane);  // next task, read at the end
             const bool hs = (int)o < nsp, ho = (int)o < nol;  // wave-uniform
             const int Wn = nol <= 64 ? __builtin_amdgcn_readlane(winreg, (int)o & 63) : win[o];
-            const int pj = ring_back(ptop, Wn, R);
             // unconditional reads at clamped / valid addresses (a task without a span or a window
             // leaves them unused): no select on the task's kind, which the compiler builds as a
             // VGPR bool
-            const double e = E[min((int)o, nsp - 1) * kEStride + lane];
-            const uint64_t r1j = r1[pj], r2j = r2[pj];
+            const int erow = min((int)o, nsp - 1) * kEStride + lane;
+            double e[TS];
+            uint64_t r1j[TS], r2j[TS];
+#pragma unroll
+            for (int u = 0; u < TS; ++u) {
+                const int pj = ring_back(pt[u], Wn, R);
+                e[u] = Er[u][erow];
+                r1j[u] = r1[pj];
+                r2j[u] = r2[pj];
+            }
             if (hs) {  // span: entry / exit conditions against the EMA
-                const uint64_t wa = __ballot(lhs < e * lo_mult), wb = __ballot(lhs > e * hi_mult);
-                const uint64_t wx = __ballot(cd >= e), wy = __ballot(cd <= e);
-                if (lane == 0) {
-                    Wd[4 * o + 0] = wa;
-                    Wd[4 * o + 1] = wb;
-                    Wd[4 * o + 2] = wx;
-                    Wd[4 * o + 3] = wy;
+#pragma unroll
+                for (int u = 0; u < TS; ++u) {
+                    const uint64_t wa = __ballot(lhs[u] < e[u] * lo_mult), wb = __ballot(lhs[u] > e[u] * hi_mult);
+                    const uint64_t wx = __ballot(cd[u] >= e[u]), wy = __ballot(cd[u] <= e[u]);
+                    if (lane == 0 && u < nt) {
+                        Wd[u][4 * o + 0] = wa;
+                        Wd[u][4 * o + 1] = wb;
+                        Wd[u][4 * o + 2] = wx;
+                        Wd[u][4 * o + 3] = wy;
+                    }
                 }
             }
             if (ho) {  // OLS window: N = 2 T - (w-1) S over [t-w+1, t], exact modulo 2^64
-                const int jj = t + 1 - Wn;
-                const uint64_t vm = vcmp_le_i32(Wn, t + 1) & tin;  // jj >= 0 && t < B
-                // 2 (sum i c_i - jj S) - (w - 1) S with one multiply
-                const uint64_t S = P1t - r1j;
-                const int64_t N = (int64_t)(2 * (P2t - r2j) - (uint64_t)(int64_t)(2 * jj + Wn - 1) * S);
-                // (masks straight from the compares: a ballot of `valid && N >= 0` is a VGPR bool
+                // 2 (sum i c_i - jj S) - (w - 1) S with one multiply, jj = t + 1 - w; masks
+                // straight from the compares (a ballot of `valid && N >= 0` is a VGPR bool
                 // compared again)
-                const uint64_t wp = vcmp_ge0_i64(N) & vm, wn = vcmp_le0_i64(N) & vm;
-                if (lane == 0) {
-                    Wd[4 * nsp + 2 * o] = wp;
-                    Wd[4 * nsp + 2 * o + 1] = wn;
+#pragma unroll
+                for (int u = 0; u < TS; ++u) {
+                    const int t = (T0 + u) * kTile + lane;
+                    const uint64_t S = P1[u] - r1j[u];
+                    const int64_t N = (int64_t)(2 * (P2[u] - r2j[u]) - (uint64_t)(int64_t)(2 * (t + 1 - Wn) + Wn - 1) * S);
+                    const uint64_t vm = vcmp_le_i32(Wn, t + 1) & tin[u];  // jj >= 0 && t < B
+                    const uint64_t wp = vcmp_ge0_i64(N) & vm, wn = vcmp_le0_i64(N) & vm;
+                    if (lane == 0 && u < nt) {
+                        Wd[u][4 * nsp + 2 * o] = wp;
+                        Wd[u][4 * nsp + 2 * o + 1] = wn;
+                    }
                 }
             }
-            o = grab_value(vn) - base;
+            o = grab_value(vn) - base - (DSTT ? TS : 0);
         }
     };
 
-    // prologue: scan + chain the first two tiles; words of the first
+    // prologue: scan + chain stages 0 and 1; tables and words of stage 0
+    int32_t cpre[TS];  // closes of the helpers' next stage, loaded a stage ahead
     if (helperA || helperB) {
         const int b0 = T_scan * kTile;
-        const int32_t c0 = ldc(crow, B, b0 + lane, 0), c1 = ldc(crow, B, b0 + kTile + lane, 0);
-        cpre = ldc(crow, B, b0 + 2 * kTile + lane, 0);
-        if (T_scan < T_end) {
-            if (helperA) scan(T_scan, c0); else chain(T_scan, c0);
-        }
-        if (T_scan + 1 < T_end) {
-            if (helperA) scan(T_scan + 1, c1); else chain(T_scan + 1, c1);
+        int32_t c0[2 * TS];
+#pragma unroll
+        for (int u = 0; u < 2 * TS; ++u) c0[u] = ldc(crow, B, b0 + u * kTile + lane, 0);
+#pragma unroll
+        for (int u = 0; u < TS; ++u) cpre[u] = ldc(crow, B, b0 + (2 * TS + u) * kTile + lane, 0);
+#pragma unroll
+        for (int u = 0; u < 2 * TS; ++u) {
+            if (T_scan + u < T_end) {
+                if (helperA) scan(T_scan + u, c0[u]); else chain(T_scan + u, c0[u]);
+            }
         }
     }
     __syncthreads();
-    if (T_scan < T_end) flags(T_scan);
+    if (helperA && !DSCAN && !DSTT) {
+#pragma unroll
+        for (int u = 0; u < TS; ++u)
+            if (T_scan + u < T_end) dbuild(T_scan + u);
+    }
+    if (nstage > 0) flags(0);
     __syncthreads();
 
     TradeAcct a;
@@ -585,14 +681,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int cap = out.trade_cap;
 
     StampAcc sa;
-    if (STAMPS) sa.begin();
-    for (int k = T_scan; k < T_end; ++k) {
+    // the walk of tile k (parameter waves)
+    auto walk = [&](int k) {
         const int t0 = k * kTile;
-        if ((helperA || helperB) && k + 2 < T_end) {
-            if (helperA) scan(k + 2, cpre); else chain(k + 2, cpre);
-            cpre = ldc(crow, B, t0 + 3 * kTile + lane, 0);
-        }
-        if (STAMPS) sa.mark(0);
         if (SEG && k == T_acct && active) {
             start_pos = a.pos;
             start_e = a.e;
@@ -600,11 +691,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         }
         if (active && k >= T_walk && !BT_ABL(g, 8)) {
             set_prio(BT_PRIO(g, 18, kEmaWalkPrio));  // the walk is the per-tile critical path
-            const int s = k % kTileStages;
+            const int s = k % CT;
             const int32_t* cT = cts + s * kTile;
             const int64_t* ql = qls + s * 2 * kTile;
-            const Agg* D = dst + s * kDstLevels * kTile;
-            const uint64_t* W = words + (k & 1) * nword;
+            const Agg* D = dst + (k % DS) * kDstLevels * kTile;
+            const uint64_t* W = words + (k % SL) * nword;
             const uint64_t vm = bar_range_mask(t0, warm, B - 2);
             const uint64_t Aw = W[4 * i_n] & W[4 * nsp + 2 * i_w] & vm;
             const uint64_t Bw = W[4 * i_n + 1] & W[4 * nsp + 2 * i_w + 1] & vm & ~Aw;
@@ -696,7 +787,31 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
             acct_tile_end(a, D, ql);
             __builtin_amdgcn_s_setprio(0);
         }
-        if (k + 1 < T_end && !BT_ABL(g, 2)) flags(k + 1);
+    };
+
+    if (STAMPS) sa.begin();
+    for (int st = 0; st < nstage; ++st) {
+        const int k0 = T_scan + TS * st;
+        if (helperA || helperB) {
+#pragma unroll
+            for (int u = 0; u < TS; ++u) {
+                const int T = k0 + 2 * TS + u;
+                if (T < T_end) {
+                    if (helperA) scan(T, cpre[u]); else chain(T, cpre[u]);
+                }
+                cpre[u] = ldc(crow, B, (T + TS) * kTile + lane, 0);
+            }
+            if (helperA && !DSCAN && !DSTT) {
+#pragma unroll
+                for (int u = 0; u < TS; ++u)
+                    if (k0 + TS + u < T_end) dbuild(k0 + TS + u);
+            }
+        }
+        if (STAMPS) sa.mark(0);
+#pragma unroll
+        for (int u = 0; u < TS; ++u)
+            if (k0 + u < T_end) walk(k0 + u);
+        if (st + 1 < nstage && !BT_ABL(g, 2)) flags(st + 1);
         if (STAMPS) sa.mark(2);
         __syncthreads();
         if (STAMPS) sa.barrier();
@@ -1251,12 +1366,16 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
     // given D / ql of its tile and the trade's sparse-table query index qi (the bar before a
     // fill, the exit bar of a signal exit): the path is the carried aggregate (kAggId for a
     // trade opened in this tile), the tile's closes [a.sb, qi] and the fill price.
-    auto close_trade = [&](auto narrow_tag, Acct32& n32, int t0, int x, int qi, int32_t px,
-                           const Agg& seg, int64_t qx, int64_t q2x) {
+    // FIRST: the tile's first record, the only one that can close a position carried in (path
+    // a.agg, and qi < a.sb for a fill at the tile's first bar); every later record closes the
+    // trade it opened (a.agg = kAggId, qi >= a.sb), whose path is the tile's closes alone.
+    auto close_trade = [&](auto narrow_tag, auto first_tag, Acct32& n32, int t0, int x, int qi,
+                           int32_t px, const Agg& seg, int64_t qx, int64_t q2x) {
         constexpr bool NARROW = decltype(narrow_tag)::value;
+        constexpr bool FIRST = decltype(first_tag)::value;
         const bool lg = a.pos > 0;
-        const Agg sp = qi < a.sb ? kAggId : seg;
-        const Agg st = agg_merge(agg_merge(a.agg, sp), agg_one(px));
+        const Agg sp = (FIRST && qi < a.sb) ? kAggId : seg;
+        const Agg st = agg_merge(FIRST ? agg_merge(a.agg, sp) : sp, agg_one(px));
         acct_close<PARITY, SEG, NARROW>(a, n32, t0 + x, px, st, tr, cap);
         a.ps1 += lg ? (uint64_t)qx : (uint64_t)0 - (uint64_t)qx;
         a.ps2 += (uint64_t)q2x;
@@ -1515,7 +1634,7 @@ __global__ __launch_bounds__(1024) void boll_tile_kernel(const SymDesc* __restri
                         const int64_t qx = ql[x], q2x = ql[kTile + x];
                         asm volatile("" ::"v"(cxx), "v"(qx), "v"(q2x));
                         const int32_t px = hit ? (kind == 2 ? XL : XHm1 + 1) : cxx;
-                        close_trade(narrow_tag, n32, ta, x, qi, px, seg, qx, q2x);
+                        close_trade(narrow_tag, first_tag, n32, ta, x, qi, px, seg, qx, q2x);
                     }
                 };
                 if (n > 0) {
@@ -1679,7 +1798,7 @@ static int tile_extra_waves(int used, int x) {
     return std::max(0, std::min(x, 16 - used));
 }
 
-size_t ema_lds_bytes(const Grid& g) { return tile_lds_layout(0, g.ring, g.na, g.nb).total; }
+size_t ema_lds_bytes(const Grid& g, int ts) { return tile_lds_layout(0, g.ring, g.na, g.nb, 0, ts).total; }
 size_t boll_lds_bytes(const Grid& g) {
     return tile_lds_layout(1, g.ring, g.na, g.nb, g.nc + g.nd).total;
 }
@@ -1703,35 +1822,63 @@ int32_t ema_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
     return G;
 }
 
-hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
-                          const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
-    if (n_sym <= 0) return hipSuccess;
+// Tiles per stage of an unsplit EMA+OLS launch: 128-bar stages (TS = 2) when they keep as many
+// blocks per CU as 64-bar ones (config 3: 80.2 KB vs 60.1 KB, two either way), else TS = 1.
+int ema_stage_tiles(const Grid& g) {
+#ifdef BT_EMA_FORCE_TS1
+    return 1;  // (A/B aid)
+#endif
+    const size_t cu = 160 * 1024, l1 = ema_lds_bytes(g, 1), l2 = ema_lds_bytes(g, 2);
+    return l2 <= cu && cu / l2 >= cu / l1 ? 2 : 1;
+}
+
+template <int TS>
+static hipError_t launch_ema_ts(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                                const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
     const int lpw = tile_lanes_per_wave();
     const int pw = tile_param_waves((g.n_params + lpw - 1) / lpw, 1024 / 64 - 2);
     const int xw = tile_extra_waves(pw + 2, 5);
     const bool split = seg.G > 1 && !parity;
     const dim3 grid(n_sym, (g.n_params + lpw * pw - 1) / (lpw * pw), split ? seg.G : 1);
     const dim3 block(64 * (pw + 2 + xw));
-    const size_t lds = ema_lds_bytes(g);
+    const size_t lds = ema_lds_bytes(g, TS);
 #ifdef BT_PROFILING
-    if (BT_ABL(g, 64)) {
-        hipLaunchKernelGGL((ema_tile_kernel<false, true, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+    if (BT_ABL(g, 64) && !split) {
+        hipLaunchKernelGGL((ema_tile_kernel<false, true, false, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
         return hipGetLastError();
     }
 #endif
     if (split) {
-        hipLaunchKernelGGL((ema_tile_kernel<false, false, true>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
-        const dim3 fgrid(grid.x, grid.y, 1);
-        for (int s = 1; s < seg.G; ++s)
-            hipLaunchKernelGGL((ema_tile_kernel<false, false, true>), fgrid, block, lds, st, syms, close, g, out, xw, lpw, seg, s);
-        const size_t n = (size_t)n_sym * g.n_params;
-        hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
+        // speculative segments (stamped in the profiling build), the fix pass of each boundary,
+        // the fold; bar segments run kEmaSegTS tiles per stage (launch_ema_ols)
+        if constexpr (TS == kEmaSegTS) {
+#ifdef BT_PROFILING
+            if (BT_ABL(g, 64))
+                hipLaunchKernelGGL((ema_tile_kernel<false, true, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+            else
+#endif
+                hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+            const dim3 fgrid(grid.x, grid.y, 1);
+            for (int s = 1; s < seg.G; ++s)
+                hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), fgrid, block, lds, st, syms, close, g, out, xw, lpw, seg, s);
+            const size_t n = (size_t)n_sym * g.n_params;
+            hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
+        }
     } else if (parity) {
-        hipLaunchKernelGGL((ema_tile_kernel<true, false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((ema_tile_kernel<true, false, false, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
     } else {
-        hipLaunchKernelGGL((ema_tile_kernel<false, false, false>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+        hipLaunchKernelGGL((ema_tile_kernel<false, false, false, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
+                          const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
+    if (n_sym <= 0) return hipSuccess;
+    const bool split = seg.G > 1 && !parity;
+    if (split) return launch_ema_ts<kEmaSegTS>(syms, n_sym, close, g, out, parity, seg, st);
+    return ema_stage_tiles(g) == 2 ? launch_ema_ts<2>(syms, n_sym, close, g, out, parity, seg, st)
+                                   : launch_ema_ts<1>(syms, n_sym, close, g, out, parity, seg, st);
 }
 
 // Bar segments per symbol for a shard of n_sym symbols: a shard with no more blocks than CUs

@@ -17,6 +17,12 @@ ntiles = (bars + 63) // 64
 e = D.Engine(grid, timing=True)
 e.load_synthetic(0x5EED, 0, S, bars, D.BT_MINUTE)
 e.run(); e.sync()
+G = e.last_segments()
+if G > 1:  # split run (speculative pass stamped): tiles per block incl. burn-in and lookback
+    burn = max(64, (6 * max(grid.axes[0]) + 63) // 64) if cfg == 3 else 64
+    look = (max(grid.axes[1] if cfg == 3 else grid.axes[0]) - 1 + 63) // 64
+    ntiles = (ntiles + (G - 1) * (burn + look)) / G
+    print(f"split run: {G} segments, ~{ntiles:.0f} tiles per block")
 buf = (C.c_uint64 * 80)()
 L.bt_read_debug(e._h, buf, 80)
 roles = (("param waves", "helper A (scan)", "helper B (chain)", "task waves") if cfg == 3 else

@@ -359,6 +359,27 @@ def test_spec_maximum_windows(strategy):
             compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
 
 
+@pytest.mark.parametrize("ols", [[1560, 15], [1700, 30]])
+def test_ema_stage_shapes(ols):
+    """EMA+OLS unsplit launches run 128-bar stages when they keep two blocks per CU (config 3's
+    1,560-bar OLS window: 80.2 KB of LDS, at the edge) and 64-bar stages otherwise (a 1,700-bar
+    window: 82.1 KB would leave one block per CU; k_tile.hip ema_stage_tiles): both shapes, with
+    windows that reach back across stages and a ragged last stage, against the oracle."""
+    grid = D.Grid.ema_ols([10, 780], ols, band_bps=20)
+    bars = 5000 + 64 * 3 + 17
+    o, h, lo, c = _gen(0x5EED, [4, 5], bars, 1)
+    with D.Engine(grid, parity=True, trade_cap=CAP) as e:
+        e.load_synthetic(0x5EED, 4, 2, bars, D.BT_MINUTE)
+        e.run()
+        got, tr = e.summaries(), e.trades()
+    for s in range(2):
+        orc, otr = oracle_row("ema_ols", grid, (o[s], h[s], lo[s], c[s]), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"ema stages ols {ols} sym {s} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)
+
+
 def test_pipelined_topk_fetch():
     """bench.py's pipelining: runs i+1 .. i+depth are enqueued before run i's top-k is read;
     each slot must hold its own run's records and trade count (same as the synchronous read of
