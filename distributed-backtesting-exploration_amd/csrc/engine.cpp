@@ -194,11 +194,7 @@ std::string validate_and_copy(bt_engine* e, const bt_config& c) {
             e->grid.wmax = *std::max_element(e->ax[1].begin(), e->ax[1].end());
             // prefix ring, a multiple of the tile (k_tile.hip): a window back from the stage
             // being flagged, which ends two 128-bar stages before the last scanned bar
-#ifdef BT_EMA_RING_OLD
-            e->grid.ring = (e->grid.wmax + 4 * kTile - 1) / kTile * kTile;  // (A/B aid: 64-bar stages only)
-#else
             e->grid.ring = (e->grid.wmax + 5 * kTile - 1) / kTile * kTile;
-#endif
             if (ema_lds_bytes(e->grid, 1) > 160 * 1024) return "EMA grid needs more LDS than a CU has (OLS windows too long)";
             break;
         }

@@ -63,22 +63,8 @@ __host__ __device__ constexpr int ema_slots(int ts) { return 2 * ts; }
 // drawdown tables: 64-bar stages build them in the scan (three stages of buffers, as the closes),
 // 128-bar stages a stage later (two)
 __host__ __device__ constexpr int ema_dst_slots(int ts) { return ts == 1 ? ema_ct_slots(1) : ema_slots(ts); }
-// 128-bar stages (TS = 2) for unsplit runs; bar segments (SEG) keep 64-bar stages
-#ifndef BT_EMA_SEG_TS
-#define BT_EMA_SEG_TS 1
-#endif
-constexpr int kEmaTS = 2, kEmaSegTS = BT_EMA_SEG_TS;
-// with 128-bar stages the drawdown tables of a stage are the first tasks of the round that flags
-// it (helper A, which scans, then has only the scans): config 3 task waves were idle ~2.5k
-// cycles per tile while helper A paced at ~3.9k
-#ifndef BT_EMA_DST_TASK
-#define BT_EMA_DST_TASK 1
-#endif
-constexpr bool kEmaDstTask = BT_EMA_DST_TASK;
-#ifndef BT_EMA_CHAIN_TASKS
-#define BT_EMA_CHAIN_TASKS 0
-#endif
-constexpr bool kEmaChainTasks = BT_EMA_CHAIN_TASKS;
+constexpr int kEmaTS = 2;  // 128-bar stages where the LDS allows (ema_stage_tiles)
+
 // Trade records per lane and tile: an entry needs a bar after the previous exit and an exit a bar
 // after its entry, so a tile holds at most 32 entries plus the exit of a position carried in.
 constexpr int kRecCap = 33;
@@ -319,9 +305,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const TileLds LL = tile_lds_layout(0, R, nsp, nol, 0, TS);
     static_assert(TS == 1 || TS == 2, "64- or 128-bar stages");
     constexpr int CT = ema_ct_slots(TS), SL = ema_slots(TS), DS = ema_dst_slots(TS);
-    // drawdown tables: built by the scan from its registers (64-bar stages), as the first tasks
-    // of the round that flags their stage (DSTT), or by helper A a stage after the scan
-    constexpr bool DSCAN = TS == 1, DSTT = kEmaDstTask && TS == 2;
+    // drawdown tables: built by the scan from its registers (64-bar stages, DSCAN), or as the
+    // first tasks of the round that flags their stage (128-bar stages, DSTT: helper A then has
+    // only the scans; config 3's task waves were idle ~2.5k cycles per tile while helper A paced
+    // at ~3.9k with the tables)
+    constexpr bool DSCAN = TS == 1, DSTT = TS == 2;
     uint64_t* r1 = reinterpret_cast<uint64_t*>(smem + LL.r1);  // sum_{i<x} c_i
     uint64_t* r2 = reinterpret_cast<uint64_t*>(smem + LL.r2);  // sum_{i<x} i*c_i (mod 2^64)
     int32_t* cts = reinterpret_cast<int32_t*>(smem + LL.ct);
@@ -351,21 +339,22 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int estage = nsp * kEStride;
 
     SegRange sr{0, 0, 0, 0, ntiles};
-    const SegRec* prev = nullptr;
-    SegRec* mine = nullptr;
     double* ema_mine = nullptr;        // this (segment, symbol)'s chain record
     const double* ema_prev = nullptr;  // the previous segment's
+    // this lane's record of segment sq, its address recomputed where it is used from an opaque
+    // copy of the parameter index (a pointer kept live across the walk costs a VGPR pair, and the
+    // split kernel runs at the 128-VGPR edge)
+    auto seg_rec = [&](int sq) {
+        int pje = pj;
+        asm volatile("" : "+v"(pje));
+        return sg.rec + (size_t)sq * gridDim.x * P + (size_t)blockIdx.x * P + pje;
+    };
     if (SEG) {
         sr = seg_range(sg, fix_seg, ntiles, g.wmax);
-        const size_t per_seg = (size_t)gridDim.x * P;
-        mine = sg.rec + sr.seg * per_seg + (size_t)blockIdx.x * P + pj;
         ema_mine = sg.ema + ((size_t)sr.seg * gridDim.x + blockIdx.x) * kEmaSegStride;
-        if (sr.seg > 0) {
-            prev = mine - per_seg;
-            ema_prev = ema_mine - (size_t)gridDim.x * kEmaSegStride;
-        }
+        if (sr.seg > 0) ema_prev = ema_mine - (size_t)gridDim.x * kEmaSegStride;
         if (fix_seg > 0) {  // re-walk if a lane's state or a span's chain value is not the true one
-            const bool lane_differs = active && seg_start_differs(mine, prev);
+            const bool lane_differs = active && seg_start_differs(seg_rec(sr.seg), seg_rec(sr.seg - 1));
             const bool chain_differs = helperB && lane < nsp && ema_mine[lane] != ema_prev[64 + lane];
             if (!__syncthreads_or(lane_differs || chain_differs)) return;
             if (tid == 0) atomicAdd(sg.refixed, 1ULL);
@@ -439,10 +428,10 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         // task rounds are numbered by stage (flags), from 0
         *ctr = 0;
     }
-    double alpha = 0.0, ema = 0.0, ema_start = 0.0;
+    double alpha = 0.0, ema = 0.0;
     if (helperB && lane < nsp) {
         alpha = 2.0 / ((double)g.a[lane] + 1.0);
-        if (chain_injected) ema = ema_start = ema_prev[64 + lane];
+        if (chain_injected) ema = ema_prev[64 + lane];
     }
     const int winreg = lane < nol ? g.b[lane] : 1;  // OLS window lengths, lane = window
     const double lo_mult = (double)(10000 - g.band_bps), hi_mult = (double)(10000 + g.band_bps);
@@ -459,13 +448,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
 
     // Stages of TS tiles (TS = 2: 128 bars per barrier): stage st holds tiles T_scan + TS st ..
     // T_scan + TS st + TS - 1 (those past T_end absent). Per stage, one barrier:
-    //   helper A: scans stage st + 2 (closes, returns, prefix rings) and, unless the tables are
-    //             tasks (DSTT), builds the drawdown tables of stage st + 1 from its staged closes (a
-    //             stage after the scan, so the tables need two stages of buffers, not three: 80 KB
-    //             per block at TS = 2);
+    //   helper A: scans stage st + 2 (closes, returns, prefix rings; at TS = 1 the drawdown
+    //             tables too);
     //   helper B: chains stage st + 2;
-    //   the other waves: the tasks of stage st + 1 (DSTT: its tables, then one task per span /
-    //             window over all its tiles);
+    //   the other waves: the tasks of stage st + 1 (DSTT: its tables, a stage after the scan,
+    //             so they need two stages of buffers, not three: 80 KB per block at TS = 2; then
+    //             one task per span / window over all its tiles);
     //   parameter waves: walk stage st, tile by tile.
     // Buffers by tile T: closes, returns, narrow flags T % CT (written st + 2, read st + 1 and st);
     // tables, chain values, words T % SL.
@@ -540,7 +528,11 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                     E[b] = ema;
                 }
             }
-            if (SEG && T + 1 == T_acct) ema_start = ema;  // the values entering the first accounted bar
+            // the values entering the first accounted bar, stored when the chain reaches them (a
+            // register kept across the walk for them costs two VGPRs at the split kernel's edge);
+            // a fix pass leaves the start record alone (other blockIdx.y blocks of the symbol
+            // compare it with the previous segment's end, chain_differs, and may not have yet)
+            if (SEG && fix_seg == 0 && T + 1 == T_acct) ema_mine[lane] = ema;
         }
         __builtin_amdgcn_s_setprio(0);
     };
@@ -549,8 +541,8 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     // critical path (config 3: ~3.7k of ~4.9k cycles per tile on the parameter wave)
     const bool walk_only = nextra >= 2;
     // ... and helper B (the chain, which sets the stage with task waves idle) takes none either:
-    // its grab after the chain would only find the round empty
-    const bool chain_only = walk_only && !kEmaChainTasks;
+    // its grab after the chain would only find the round empty (DESIGN.md §0.0 E4)
+    const bool chain_only = walk_only;
     const bool no_tasks = (walk_only && wave < npw) || (chain_only && helperB);
     const int ngrab = nwaves - (walk_only ? npw : 0) - (chain_only ? 1 : 0);
 
@@ -660,22 +652,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
         }
     }
     __syncthreads();
-    if (helperA && !DSCAN && !DSTT) {
-#pragma unroll
-        for (int u = 0; u < TS; ++u)
-            if (T_scan + u < T_end) dbuild(T_scan + u);
-    }
     if (nstage > 0) flags(0);
     __syncthreads();
 
     TradeAcct a;
     acct_init(a);
-    int32_t start_pos = 0, start_e = 0;  // SEG: state at the first accounted bar
-    if (SEG && fix_seg > 0 && active) {
-        seg_inject(a, prev);
-        start_pos = a.pos;
-        start_e = a.e;
-    }
+    if (SEG && fix_seg > 0 && active) seg_inject(a, seg_rec(sr.seg - 1));
     const size_t gi = (size_t)blockIdx.x * P + pj;
     bt_trade* tr = (PARITY && active) ? out.trades + gi * out.trade_cap : nullptr;
     const int cap = out.trade_cap;
@@ -685,8 +667,9 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     auto walk = [&](int k) {
         const int t0 = k * kTile;
         if (SEG && k == T_acct && active) {
-            start_pos = a.pos;
-            start_e = a.e;
+            // first accounted tile: the state the (speculative) walk reached goes to the record
+            // now; the burn-in's sums are dropped
+            seg_write_start(seg_rec(sr.seg), a.pos, a.e);
             seg_reset_sums(a);
         }
         if (active && k >= T_walk && !BT_ABL(g, 8)) {
@@ -801,11 +784,6 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
                 }
                 cpre[u] = ldc(crow, B, (T + TS) * kTile + lane, 0);
             }
-            if (helperA && !DSCAN && !DSTT) {
-#pragma unroll
-                for (int u = 0; u < TS; ++u)
-                    if (k0 + TS + u < T_end) dbuild(k0 + TS + u);
-            }
         }
         if (STAMPS) sa.mark(0);
 #pragma unroll
@@ -818,12 +796,15 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     }
     if (STAMPS) sa.flush(out.dbg, wave < npw ? 0 : (helperA ? 1 : (helperB ? 2 : 3)), lane);
     if (SEG) {
-        if (active) seg_write(a, start_pos, start_e, mine);
+        if (active) {
+            // a segment with no bars never reached its first accounted tile: the state passes
+            // through (flat, or the fix pass's injected one)
+            if (T_acct >= T_end) seg_write_start(seg_rec(sr.seg), a.pos, a.e);
+            seg_write_rest(a, seg_rec(sr.seg));
+        }
         if (helperB && lane < nsp) {
-            // the start record is written by the speculative pass only: a fix pass must leave it
-            // alone, because the other blockIdx.y blocks of this symbol compare it with the
-            // previous segment's end (chain_differs) and may not have done so yet
-            if (fix_seg == 0) ema_mine[lane] = ema_start;
+            // a speculative segment whose chain never reached its first accounted bar records 0
+            if (fix_seg == 0 && !(T_acct >= T_scan + 1 && T_acct <= T_end)) ema_mine[lane] = 0.0;
             ema_mine[64 + lane] = ema;  // after the segment's last bar
         }
         return;
@@ -1822,12 +1803,9 @@ int32_t ema_auto_segments(int32_t n_sym, int32_t n_params, int32_t max_bars, int
     return G;
 }
 
-// Tiles per stage of an unsplit EMA+OLS launch: 128-bar stages (TS = 2) when they keep as many
-// blocks per CU as 64-bar ones (config 3: 80.2 KB vs 60.1 KB, two either way), else TS = 1.
+// Tiles per stage of an EMA+OLS launch: 128-bar stages (TS = 2) when they keep as many blocks per
+// CU as 64-bar ones (config 3: 80.2 KB vs 61.1 KB, two either way), else TS = 1.
 int ema_stage_tiles(const Grid& g) {
-#ifdef BT_EMA_FORCE_TS1
-    return 1;  // (A/B aid)
-#endif
     const size_t cu = 160 * 1024, l1 = ema_lds_bytes(g, 1), l2 = ema_lds_bytes(g, 2);
     return l2 <= cu && cu / l2 >= cu / l1 ? 2 : 1;
 }
@@ -1850,20 +1828,18 @@ static hipError_t launch_ema_ts(const SymDesc* syms, int32_t n_sym, const int32_
 #endif
     if (split) {
         // speculative segments (stamped in the profiling build), the fix pass of each boundary,
-        // the fold; bar segments run kEmaSegTS tiles per stage (launch_ema_ols)
-        if constexpr (TS == kEmaSegTS) {
+        // the fold
 #ifdef BT_PROFILING
-            if (BT_ABL(g, 64))
-                hipLaunchKernelGGL((ema_tile_kernel<false, true, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
-            else
+        if (BT_ABL(g, 64))
+            hipLaunchKernelGGL((ema_tile_kernel<false, true, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+        else
 #endif
-                hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
-            const dim3 fgrid(grid.x, grid.y, 1);
-            for (int s = 1; s < seg.G; ++s)
-                hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), fgrid, block, lds, st, syms, close, g, out, xw, lpw, seg, s);
-            const size_t n = (size_t)n_sym * g.n_params;
-            hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
-        }
+            hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
+        const dim3 fgrid(grid.x, grid.y, 1);
+        for (int s = 1; s < seg.G; ++s)
+            hipLaunchKernelGGL((ema_tile_kernel<false, false, true, TS>), fgrid, block, lds, st, syms, close, g, out, xw, lpw, seg, s);
+        const size_t n = (size_t)n_sym * g.n_params;
+        hipLaunchKernelGGL(seg_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, syms, n_sym, g.n_params, seg.rec, seg.G, g.sqrt_ann, out);
     } else if (parity) {
         hipLaunchKernelGGL((ema_tile_kernel<true, false, false, TS>), grid, block, lds, st, syms, close, g, out, xw, lpw, seg, 0);
     } else {
@@ -1875,8 +1851,6 @@ static hipError_t launch_ema_ts(const SymDesc* syms, int32_t n_sym, const int32_
 hipError_t launch_ema_ols(const SymDesc* syms, int32_t n_sym, const int32_t* close, const Grid& g,
                           const Out& out, bool parity, const SegArgs& seg, hipStream_t st) {
     if (n_sym <= 0) return hipSuccess;
-    const bool split = seg.G > 1 && !parity;
-    if (split) return launch_ema_ts<kEmaSegTS>(syms, n_sym, close, g, out, parity, seg, st);
     return ema_stage_tiles(g) == 2 ? launch_ema_ts<2>(syms, n_sym, close, g, out, parity, seg, st)
                                    : launch_ema_ts<1>(syms, n_sym, close, g, out, parity, seg, st);
 }
