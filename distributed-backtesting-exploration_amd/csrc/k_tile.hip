@@ -35,10 +35,12 @@ namespace {
 
 // wave priorities (s_setprio) of the pacing roles; BT_PRIO overrides them in the profiling build
 // (scripts/gpu_prio_sweep.sh). Round 3 sweep + release A/B: the accountant one level below the
-// finder, 7.23 -> 7.03 ms on config 4 at 500 symbols and 3.95 -> 3.83 at 250; the EMA chain at
-// the base priority (it raised the chain above the walk before), config 3 -0.5 to -1 %
+// finder, 7.23 -> 7.03 ms on config 4 at 500 symbols and 3.95 -> 3.83 at 250. The EMA chain at
+// the top priority since it alone sets the 128-bar stage (round 6: helper A's tables moved to
+// tasks and the chain wave out of the task rounds): config 3 2.565 -> 2.483 ms at 500 symbols,
+// 1.598 -> 1.511 at 250 (at the base priority before, -0.5 to -1 %)
 #ifndef BT_EMA_CHAIN_PRIO
-#define BT_EMA_CHAIN_PRIO 0
+#define BT_EMA_CHAIN_PRIO 3
 #endif
 #ifndef BT_EMA_WALK_PRIO
 #define BT_EMA_WALK_PRIO 2
