@@ -246,10 +246,12 @@ def main():
         else:
             eng.topk_fetch_async(slot)       # its top-k + trade count into a pinned slot
 
-    xch_s = [0.0]  # host time in the torch.distributed exchange proper (all-gather + merge)
+    xch_s = [0.0]  # host time in the torch.distributed exchange proper (issue + merge)
+    pending = [None]  # torch.distributed carrier: the exchange still in flight
 
     def finish(i):
-        """(top-k, [bar-evals, trades]) of step i over every rank."""
+        """(top-k, [bar-evals, trades]) over every rank of step i (torch.distributed carrier: of
+        step i - 1, the exchange of step i is left in flight; drain() completes it)."""
         if topk == 0:
             return None, None
         slot = i % D.PIPE_SLOTS
@@ -259,11 +261,23 @@ def main():
         if dist is None:
             return top, [n_sym * BARS * P, trades]
         # the one exchange step: a single all-gather carrying each rank's k x 24 B top-k records
-        # and its run counters (summed on the host), in the C-ABI exchange's byte format
+        # and its run counters (summed on the host), in the C-ABI exchange's byte format, issued
+        # asynchronously; the previous step's is merged now, a step after it was issued (the
+        # RCCL carrier's all-gather likewise runs behind the next step's kernel)
         tx = time.perf_counter()
-        r = PAR.exchange(top, topk, [n_sym * BARS * P, trades], dist)
+        prev, pending[0] = pending[0], PAR.exchange_async(top, topk, [n_sym * BARS * P, trades], dist)
+        r = prev.wait() if prev is not None else (None, None)
         xch_s[0] += time.perf_counter() - tx
         return r
+
+    def drain(res):
+        """The last step's exchange, if one is in flight (torch.distributed carrier)."""
+        if pending[0] is None:
+            return res
+        tx = time.perf_counter()
+        res, pending[0] = pending[0].wait(), None
+        xch_s[0] += time.perf_counter() - tx
+        return res
 
     wait_s = [0.0]  # host time blocked in finish() this run: the wait for the step's GPU work
                     # (kernel, top-k chain, read-back or RCCL all-gather) plus the exchange
@@ -282,6 +296,9 @@ def main():
             tw = time.perf_counter()
             res = finish(i)
             wait_s[0] += time.perf_counter() - tw
+        tw = time.perf_counter()
+        res = drain(res)
+        wait_s[0] += time.perf_counter() - tw
         return res
 
     steps(args.warmup)

@@ -66,6 +66,34 @@ def exchange(local: np.ndarray, k: int, counters, dist) -> tuple:
     return exchange_merge(out.cpu().numpy().tobytes(), world, k, k)
 
 
+class PendingExchange:
+    """An exchange (see `exchange`) whose all-gather is in flight: wait() returns (merged top-k,
+    summed counters). Lets a caller overlap the collective with its next step."""
+
+    def __init__(self, work, out, world, k):
+        self._work, self._out, self._world, self._k = work, out, world, k
+
+    def wait(self) -> tuple:
+        from .engine import exchange_merge
+        self._work.wait()
+        return exchange_merge(self._out.cpu().numpy().tobytes(), self._world, self._k, self._k)
+
+
+def exchange_async(local: np.ndarray, k: int, counters, dist) -> PendingExchange:
+    """`exchange` with the all-gather issued asynchronously (async_op): the same byte message
+    and merge, completed by PendingExchange.wait()."""
+    import torch
+    from .engine import exchange_message
+    world = dist.get_world_size()
+    evals, trades = (int(v) for v in counters)
+    n = min(len(local), k)
+    msg = exchange_message(np.asarray(local, TOPK_DTYPE)[:n], k, evals, trades)
+    t = torch.frombuffer(bytearray(msg), dtype=torch.uint8).to(_device_for(dist))
+    out = torch.empty(world * len(msg), dtype=torch.uint8, device=t.device)
+    work = dist.all_gather_into_tensor(out, t, async_op=True)
+    return PendingExchange(work, out, world, k)
+
+
 def make_comm(dist, device: int, k: int):
     """The C-ABI exchange (engine.Comm over RCCL) for this process group: rank 0 creates the RCCL
     unique id, the launcher's process group broadcasts it, every rank joins."""

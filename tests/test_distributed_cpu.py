@@ -46,6 +46,14 @@ def _worker(rank, world, port, q):
         # bench.py's single-collective form: same merge, same sums
         top2, tot2 = PAR.exchange(local_top, K, [count, len(local)], dist)
         assert top2.tolist() == top.tolist() and tot2 == tot
+        # ... and its asynchronous form, two in flight at once as bench.py keeps them (the
+        # second message is the first with its counters doubled)
+        p1 = PAR.exchange_async(local_top, K, [count, len(local)], dist)
+        p2 = PAR.exchange_async(local_top, K, [2 * count, 2 * len(local)], dist)
+        top3, tot3 = p1.wait()
+        top4, tot4 = p2.wait()
+        assert top3.tolist() == top.tolist() and tot3 == tot
+        assert top4.tolist() == top.tolist() and tot4 == [2 * x for x in tot]
         q.put((rank, top.tolist(), tot))
     finally:
         dist.destroy_process_group()
