@@ -452,8 +452,11 @@ void run_impl(bt_engine* e) {
         // marker less between two runs' kernels)
         if (!timing) HIPCHK(hipEventRecord(e->ev_kdone, e->stream));
         HIPCHK(hipStreamWaitEvent(e->tstream, timing ? ev.second : e->ev_kdone, 0));
+        // the chain's histograms take no LDS beside a strategy kernel whose blocks fill a CU's
+        // (EMA+OLS in 128-bar stages: k_topk.hip topk_hist_global)
+        const bool lds_free = e->grid.strategy == BT_EMA_OLS && ema_stage_tiles(e->grid) == 2;
         HIPCHK(launch_topk(e->d_key[b].p, e->d_sum[b].p, e->d_syms.p, (int64_t)S * e->P, e->P,
-                           e->cfg.topk, topk_work(e), e->tstream));
+                           e->cfg.topk, topk_work(e), e->tstream, lds_free));
         HIPCHK(hipEventRecord(e->ev_tdone[b], e->tstream));
         e->tdone_armed[b] = true;
     }

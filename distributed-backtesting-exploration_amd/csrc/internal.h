@@ -171,7 +171,7 @@ struct TopkWork {
     int32_t* out_n;                // [1]: records written, -1 = overflow (host finishes)
 };
 hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms,
-                       int64_t n, int32_t P, int32_t k, const TopkWork& w, hipStream_t st);
+                       int64_t n, int32_t P, int32_t k, const TopkWork& w, hipStream_t st, bool lds_free_hist = false);
 hipError_t launch_topk_init(const TopkWork& w, hipStream_t st);  // once per buffer allocation
 
 // Host-side pieces shared by engine.cpp and comm.cpp.

@@ -17,6 +17,8 @@ namespace bt {
 
 namespace {
 constexpr int kBins = 4096;
+// key counts up to which the histogram passes use global atomics only (topk_hist_global)
+constexpr int64_t kHistGlobalMax = 1 << 18;
 }
 
 // state: [0] prefix, [1] mask of decided bits, [2] records still needed from the prefix group
@@ -35,6 +37,26 @@ __global__ __launch_bounds__(256) void topk_hist(const uint64_t* __restrict__ ke
     __syncthreads();
     for (int i = threadIdx.x; i < kBins; i += blockDim.x)
         if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// The same histogram without LDS: every matching key adds to the global bins directly. Used (up
+// to kHistGlobalMax keys) behind a strategy kernel whose two blocks per CU fill the LDS (EMA+OLS
+// in 128-bar stages: 2 x 80.2 KB), so that the chain's first kernel never takes LDS from a CU
+// and both blocks can always be placed, whichever is dispatched first when a run ends: a 16-KB
+// histogram block placed first split a CU's free LDS so that its second block waited for the
+// first to finish, and the kernel ran up to 1.9x longer (profiles/r06/topk_lds_race.txt). Not
+// by default: beside the Bollinger kernel (26 KB spare per CU) the global atomics on its 128k
+// keys' few hot bins made the kernel 7 % slower.
+__global__ __launch_bounds__(256) void topk_hist_global(const uint64_t* __restrict__ key, int64_t n,
+                                                        int shift,
+                                                        const unsigned long long* __restrict__ state,
+                                                        unsigned int* __restrict__ hist) {
+    const uint64_t prefix = state[0], mask = state[1];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = key[i];
+        if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & (kBins - 1)], 1u);
+    }
 }
 
 // One block of 256 threads; thread t owns bins 4095-16t .. 4080-16t (counted from the top).
@@ -316,7 +338,7 @@ hipError_t launch_topk_init(const TopkWork& w, hipStream_t st) {
 // The chain assumes the state left by topk_init or by the previous chain's finish; the
 // histogram is left zeroed by topk_select.
 hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc* syms, int64_t n,
-                       int32_t P, int32_t k, const TopkWork& w, hipStream_t st) {
+                       int32_t P, int32_t k, const TopkWork& w, hipStream_t st, bool lds_free_hist) {
     if (n <= 0 || k <= 0) return hipSuccess;
     const unsigned long long need = (unsigned long long)(k < n ? k : n);
     // few blocks, many keys per thread: each block adds its LDS histogram's non-empty bins to the
@@ -325,8 +347,12 @@ hipError_t launch_topk(const uint64_t* key, const bt_summary* sum, const SymDesc
     int64_t blocks = (n + 8191) / 8192;
     if (blocks > 256) blocks = 256;
     for (int shift = 52; shift >= 40; shift -= 12) {
-        hipLaunchKernelGGL(topk_hist, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
-                           (const unsigned long long*)w.state, w.hist);
+        if (lds_free_hist && n <= kHistGlobalMax)
+            hipLaunchKernelGGL(topk_hist_global, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
+                               (const unsigned long long*)w.state, w.hist);
+        else
+            hipLaunchKernelGGL(topk_hist, dim3((unsigned)blocks), dim3(256), 0, st, key, n, shift,
+                               (const unsigned long long*)w.state, w.hist);
         hipLaunchKernelGGL(topk_select, dim3(1), dim3(256), 0, st, w.hist, shift, w.state,
                            shift == 52 ? need : 0ULL);
     }
