@@ -7,8 +7,14 @@ parity cases must hold both shapes often:
 * a carried position closed in a tile and further trades (or reversals) after it in the same
   tile (the non-first, merge-free walk iterations).
 
-The CPU test checks that the seeded cases below contain both shapes (oracle trade lists); the GPU
-test checks every field and trade of them bit-exact against the C oracle (oracle/oracle.c
+EMA+OLS runs 128-bar stages (two tiles per barrier) when they keep as many blocks per CU as
+64-bar ones (`k_tile.hip ema_stage_tiles`): a long OLS window (1,560 bars, config 3's) puts the
+`ema_ols_128` grid there, and its cases must also hold trades carried across a stage edge, exits
+on a stage's first bar, entries on a stage's last bar and trades across the edge between a
+stage's two tiles.
+
+The CPU tests check that the seeded cases below contain these shapes (oracle trade lists); the
+GPU test checks every field and trade of them bit-exact against the C oracle (oracle/oracle.c
 orc_boll / orc_ema_ols / orc_sma, docs/oracle_spec.md §4).
 """
 import numpy as np
@@ -37,10 +43,12 @@ GRIDS = {
     # finder and an accountant (k_tile.hip), so these shapes run through the trade records
     "boll_split": lambda: D.Grid.boll([4, 9, 30, 60], [1, 2, 4], [5, 25], [5, 40, 80], k_den=2),
     "ema_ols": lambda: D.Grid.ema_ols([3, 8, 40], [4, 16], band_bps=0),
+    # 128-bar stages: the 1,560-bar window's prefix ring makes 64-bar stages no denser in LDS
+    "ema_ols_128": lambda: D.Grid.ema_ols([3, 8, 40], [4, 16, 1560], band_bps=0),
     "sma": lambda: D.Grid.sma([2, 3, 7], [4, 11, 50]),
 }
-ANN = {"boll": 98280, "boll_split": 98280, "ema_ols": 98280, "sma": 252}
-STRATEGY = {"boll_split": "boll"}
+ANN = {"boll": 98280, "boll_split": 98280, "ema_ols": 98280, "ema_ols_128": 98280, "sma": 252}
+STRATEGY = {"boll_split": "boll", "ema_ols_128": "ema_ols"}
 
 
 def _shapes(trades, n, close):
@@ -57,7 +65,33 @@ def _shapes(trades, n, close):
     return edge_fill, carried_then_more
 
 
-@pytest.mark.parametrize("strategy", ["boll", "boll_split", "ema_ols", "sma"])
+def _stage_shapes(trades, n, S=2 * T):
+    """Trades against S-bar stage edges: (carried across a stage edge, exits on a stage's first
+    bar, entries on a stage's last bar, trades across the edge between a stage's two tiles)."""
+    cross = first = last = mid = 0
+    for t in trades[:n]:
+        e, x = int(t["entry_bar"]), int(t["exit_bar"])
+        cross += e // S < x // S
+        first += x % S == 0 and e < x
+        last += e % S == S - 1
+        mid += e // S == x // S and e % S < T <= x % S
+    return cross, first, last, mid
+
+
+def test_cases_hold_stage_edge_shapes():
+    grid = GRIDS["ema_ols_128"]()
+    tot = np.zeros(4, np.int64)
+    for seed in range(2):
+        c, hi, lo = _case(seed)
+        orc, otr = oracle_row("ema_ols", grid, (c, hi, lo, c), ANN["ema_ols_128"], CAP)
+        for p in range(grid.n_params):
+            tot += _stage_shapes(otr[p], int(orc[p]["n_trades"]))
+    cross, first, last, mid = tot.tolist()
+    assert cross >= 50 and mid >= 50, (cross, mid)
+    assert first >= 10 and last >= 10, (first, last)
+
+
+@pytest.mark.parametrize("strategy", ["boll", "boll_split", "ema_ols", "ema_ols_128", "sma"])
 def test_cases_hold_tile_edge_shapes(strategy):
     grid = GRIDS[strategy]()
     edge = more = 0
@@ -75,7 +109,7 @@ def test_cases_hold_tile_edge_shapes(strategy):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("strategy", ["boll", "boll_split", "ema_ols", "sma"])
+@pytest.mark.parametrize("strategy", ["boll", "boll_split", "ema_ols", "ema_ols_128", "sma"])
 def test_tile_edge_trades_gpu(strategy):
     grid = GRIDS[strategy]()
     cases = [_case(seed) for seed in range(2)]
