@@ -55,3 +55,22 @@ def compare_trades(gpu_tr, orc_tr, n, where=""):
     exp = [tuple(int(x) for x in (t["entry_bar"], t["exit_bar"], t["side"], t["entry_px"], t["exit_px"]))
            for t in orc_tr[:n]]
     assert got == exp, f"{where}: trade lists differ (first diff at {next((i for i,(a,b) in enumerate(zip(got,exp)) if a!=b), None)})"
+
+
+def ema_stage_tiles(spans, windows):
+    """Model of k_tile.hip ema_stage_tiles / tile_lds_layout(kind 0): the EMA+OLS block's LDS bytes
+    at 64-bar (TS 1) and 128-bar (TS 2) stages and the stage the launcher picks (TS 2 when it keeps
+    as many blocks per CU). Used only to choose test grids that reach each shape; pinned to the
+    kernel's own figures for config 3 (61,120 / 80,208 B) in test_tile_edge_trades.py."""
+    T, cu = 64, 160 * 1024
+    ring = (max(windows) + 5 * T - 1) // T * T
+    na, nb = len(spans), len(windows)
+
+    def lds(ts):
+        ns, nd, sl = 3 * ts, 3 if ts == 1 else 2 * ts, 2 * ts
+        parts = [ring * 8, ring * 8, ns * T * 4, ns * 2 * T * 8, nd * 6 * T * 16,
+                 sl * na * (T + 1) * 8, sl * (4 * na + 2 * nb) * 8, nb * 4, ns * 4, 4]
+        return sum((p + 15) & ~15 for p in parts)
+
+    l1, l2 = lds(1), lds(2)
+    return (2 if l2 <= cu and cu // l2 >= cu // l1 else 1), l1, l2

@@ -361,9 +361,11 @@ def test_spec_maximum_windows(strategy):
 
 @pytest.mark.parametrize("ols", [[1560, 15], [1700, 30]])
 def test_ema_stage_shapes(ols):
-    """EMA+OLS unsplit launches run 128-bar stages when they keep two blocks per CU (config 3's
-    1,560-bar OLS window: 80.2 KB of LDS, at the edge) and 64-bar stages otherwise (a 1,700-bar
-    window: 82.1 KB would leave one block per CU; k_tile.hip ema_stage_tiles): both shapes, with
+    """EMA+OLS launches run 128-bar stages when they keep as many blocks per CU as 64-bar ones
+    (k_tile.hip ema_stage_tiles) and 64-bar stages otherwise. With two spans, a 1,560-bar OLS
+    window gives 54.3 KB at 64-bar stages (three blocks per CU) and 66.6 KB at 128-bar (two):
+    64-bar stages; a 1,700-bar window 56.3 / 68.6 KB (two either way): 128-bar stages
+    (tests/helpers.py ema_stage_tiles, pinned in test_tile_edge_trades.py). Both shapes, with
     windows that reach back across stages and a ragged last stage, against the oracle."""
     grid = D.Grid.ema_ols([10, 780], ols, band_bps=20)
     bars = 5000 + 64 * 3 + 17

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import dbx_amd as D
-from helpers import compare_summary, compare_trades, oracle_row
+from helpers import compare_summary, compare_trades, ema_stage_tiles, oracle_row
 
 pytestmark = pytest.mark.gpu
 
@@ -120,3 +120,38 @@ def test_random_product_kernels(strategy, seed):
         orc, _ = oracle_row(strategy, grid, ohlc, ann, CAP)
         for p in range(grid.n_params):
             compare_summary(got[s, p], orc[p], f"{strategy} seed {seed} sym {s} len {len(cl)} {grid.param(p)}")
+
+
+def _ema_grid_128(rng):
+    """A random EMA+OLS grid that the launcher runs in 128-bar stages (helpers.ema_stage_tiles):
+    short random spans and windows plus one OLS window long enough (1,300-2,600 bars) that
+    64-bar stages would not fit more blocks per CU."""
+    for _ in range(64):
+        spans = _windows(rng, int(rng.integers(2, 9)), 800)
+        wins = sorted(set(_windows(rng, 3, 400) + [int(rng.integers(1300, 2600))]))
+        if ema_stage_tiles(spans, wins)[0] == 2:
+            return D.Grid.ema_ols(spans, wins, band_bps=int(rng.integers(0, 60)))
+    raise AssertionError("no 128-bar-stage grid drawn")
+
+
+@pytest.mark.parametrize("parity,seed", [(p, s) for p in (True, False) for s in range(S0, S0 + (NS or 16))])
+def test_random_ema_128bar_stages(parity, seed):
+    """The 128-bar-stage EMA+OLS kernel (config 3's shape) on random grids and ragged paths: with
+    trade lists (parity instantiation) and the release instantiation, every field vs the oracle."""
+    rng = np.random.default_rng(4000 + seed + (500 if parity else 0))
+    grid = _ema_grid_128(rng)
+    kinds = ["walk", "narrow", "plateau", "spiky"]
+    closes = [_series(rng, int(n), kinds[i % 4])
+              for i, n in enumerate(rng.choice([1, 65, 129, 640, 2000, 3000, 4500], 6))]
+    with D.Engine(grid, parity=parity, trade_cap=CAP if parity else 0) as e:
+        e.load_ohlc(closes)
+        e.run()
+        got = e.summaries()
+        tr = e.trades() if parity else None
+    for s, cl in enumerate(closes):
+        orc, otr = oracle_row("ema_ols", grid, (cl, cl, cl, cl), 98280, CAP)
+        for p in range(grid.n_params):
+            where = f"ema 128 seed {seed} sym {s} len {len(cl)} {grid.param(p)}"
+            compare_summary(got[s, p], orc[p], where)
+            if parity:
+                compare_trades(tr[s, p], otr[p], int(orc[p]["n_trades"]), where)

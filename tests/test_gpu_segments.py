@@ -7,7 +7,7 @@ import pytest
 
 import dbx_amd as D
 import orc_ffi as F
-from helpers import compare_summary, oracle_row
+from helpers import compare_summary, ema_stage_tiles, oracle_row
 
 pytestmark = pytest.mark.gpu
 
@@ -103,12 +103,16 @@ def _run_grid(grid, cols, segments, burn=0):
 
 
 @pytest.mark.parametrize("segments,burn", [(2, 0), (3, 0), (2, 1), (4, 2)])
-def test_ema_split_equals_unsplit_and_oracle(segments, burn):
+@pytest.mark.parametrize("long_window,stage", [(780, 1), (1560, 2)])
+def test_ema_split_equals_unsplit_and_oracle(segments, burn, long_window, stage):
     """EMA+OLS segments must also agree on the fp64 EMA chains at every boundary: with the
     default burn-in (6 x the longest span, the chains starting from the weighted-sum estimate)
     the speculative chains meet the true ones; with a 1-2 tile burn-in the lanes' trade states
-    (and the longest span's chain) mostly do not, and the fix pass re-walks from the true values."""
-    grid = D.Grid.ema_ols([10, 60, 390], [15, 120, 780], band_bps=20)
+    (and the longest span's chain) mostly do not, and the fix pass re-walks from the true values.
+    The 1,560-bar OLS window puts the split kernel in 128-bar stages (config 3's 250-symbol
+    shard runs so), the 780-bar one in 64-bar stages (tests/helpers.py ema_stage_tiles)."""
+    grid = D.Grid.ema_ols([10, 60, 390], [15, 120, long_window], band_bps=20)
+    assert ema_stage_tiles(*grid.axes[:2])[0] == stage
     cols = [F.gen(0x5EED, 60 + i, 40000, 1) for i in range(3)]
     ref, used1, _ = _run_grid(grid, cols, 1)
     got, used, refixed = _run_grid(grid, cols, segments, burn)
@@ -122,8 +126,10 @@ def test_ema_split_equals_unsplit_and_oracle(segments, burn):
             compare_summary(got[i, p], orc[p], f"ema G={segments} burn={burn} sym {i} {grid.param(p)}")
 
 
-def test_ema_split_ragged_and_empty_segments():
-    grid = D.Grid.ema_ols([2, 3, 10, 100], [2, 4, 70, 200], band_bps=20)
+@pytest.mark.parametrize("long_window,stage", [(200, 1), (1700, 2)])
+def test_ema_split_ragged_and_empty_segments(long_window, stage):
+    grid = D.Grid.ema_ols([2, 3, 10, 100], [2, 4, 70, long_window], band_bps=20)
+    assert ema_stage_tiles(*grid.axes[:2])[0] == stage
     lengths = [1, 2, 63, 64, 65, 130, 700, 5000]
     cols = [F.gen(0x5EED, 80 + i, n, 1) for i, n in enumerate(lengths)]
     ref, _, _ = _run_grid(grid, cols, 1)

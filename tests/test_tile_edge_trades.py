@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 import dbx_amd as D
-from helpers import compare_summary, compare_trades, oracle_row
+from helpers import compare_summary, compare_trades, ema_stage_tiles, oracle_row
 
 CAP = 8192
 T = 64
@@ -76,6 +76,18 @@ def _stage_shapes(trades, n, S=2 * T):
         last += e % S == S - 1
         mid += e // S == x // S and e % S < T <= x % S
     return cross, first, last, mid
+
+
+def test_stage_model_picks_the_kernels_shapes():
+    """helpers.ema_stage_tiles mirrors the launcher's rule: config 3's block is 61,120 B at 64-bar
+    and 80,208 B at 128-bar stages (k_tile.hip ema_stage_tiles), two per CU either way."""
+    g3 = D.config3_grid()
+    assert ema_stage_tiles(g3.axes[0], g3.axes[1]) == (2, 61120, 80208)
+    # test_ema_stage_shapes' two cases: one of each shape
+    assert ema_stage_tiles([10, 780], [1560, 15]) == (1, 54288, 66560)
+    assert ema_stage_tiles([10, 780], [1700, 30]) == (2, 56336, 68608)
+    assert ema_stage_tiles(*GRIDS["ema_ols_128"]().axes[:2])[0] == 2
+    assert ema_stage_tiles(*GRIDS["ema_ols"]().axes[:2])[0] == 1
 
 
 def test_cases_hold_stage_edge_shapes():
