@@ -121,6 +121,49 @@ __device__ __forceinline__ int64_t wave_iscan_i64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// The same scans with each step one add-with-carry pair whose first operand is the DPP-moved
+// value (v_add_co_u32_dpp / v_addc_co_u32_dpp: lanes with no source add 0, rows outside the row
+// mask keep x): the compiler's DPP combine does not reach a 64-bit add, so wave_iscan_i64 spends
+// two DPP moves, their two `old` moves and a 64-bit add per step. gfx950 needs two wait states
+// between a VALU write and a DPP read of the same VGPR: one scan pads each step with an s_nop,
+// two interleaved scans need none; every block starts and ends with one, so the code around it
+// needs no hazard tracking into the asm. Used by the EMA helper's tile scan only: there it
+// measured -1.4 % (config 3, 500 symbols), in the Bollinger and SMA kernels +0.4 to +0.9 %
+// (DESIGN.md §0.0 E11).
+#define BT_S64_CTRLS(X)                                                                   \
+    X("row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")                                \
+    X("row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1")                                \
+    X("row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")                                \
+    X("row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")                                \
+    X("row_bcast:15 row_mask:0xa bank_mask:0xf")                                          \
+    X("row_bcast:31 row_mask:0xc bank_mask:0xf")
+__device__ __forceinline__ int64_t wave_iscan_i64_ac(int64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)((uint64_t)x >> 32);
+#define BT_S64_ONE(ctrl)                                                                   \
+    "s_nop 1\n"                                                                            \
+    "v_add_co_u32_dpp %0, vcc, %0, %0 " ctrl "\n"                                          \
+    "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " ctrl "\n"
+    asm volatile(BT_S64_CTRLS(BT_S64_ONE) "s_nop 1" : "+v"(lo), "+v"(hi) : : "vcc");
+#undef BT_S64_ONE
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// two independent scans, interleaved (each DPP read three instructions after its write)
+__device__ __forceinline__ void wave_iscan2_i64_ac(int64_t& x, int64_t& y) {
+    uint32_t xl = (uint32_t)x, xh = (uint32_t)((uint64_t)x >> 32);
+    uint32_t yl = (uint32_t)y, yh = (uint32_t)((uint64_t)y >> 32);
+#define BT_S64_TWO(ctrl)                                                                   \
+    "v_add_co_u32_dpp %0, vcc, %0, %0 " ctrl "\n"                                          \
+    "v_addc_co_u32_dpp %1, vcc, %1, %1, vcc " ctrl "\n"                                    \
+    "v_add_co_u32_dpp %2, vcc, %2, %2 " ctrl "\n"                                          \
+    "v_addc_co_u32_dpp %3, vcc, %3, %3, vcc " ctrl "\n"
+    asm volatile("s_nop 1\n" BT_S64_CTRLS(BT_S64_TWO) "s_nop 1"
+                 : "+v"(xl), "+v"(xh), "+v"(yl), "+v"(yh) : : "vcc");
+#undef BT_S64_TWO
+    x = (int64_t)(((uint64_t)xh << 32) | xl);
+    y = (int64_t)(((uint64_t)yh << 32) | yl);
+}
+#undef BT_S64_CTRLS
+
 // Wave64 inclusive scan of uint32 (same DPP steps as wave_iscan_i64); lane 63 holds the total.
 __device__ __forceinline__ uint32_t wave_iscan_u32(uint32_t x) {
     x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);  // row_shr:1

@@ -462,12 +462,12 @@ __global__ __launch_bounds__(1024) void ema_tile_kernel(const SymDesc* __restric
     const int nstage = (T_end - T_scan + TS - 1) / TS;
     auto scan = [&](int T, int32_t c) {
         const int s = T % CT, t0 = T * kTile, t = t0 + lane;
-        const int64_t pre = tile_scan(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
+        int64_t inc2 = (int64_t)t * c;  // c = 0 past the end; scanned with the closes
+        const int64_t pre = tile_scan<false, true>(c, B, t0, lane, cts + s * kTile, qls + s * 2 * kTile,
                                       dst + (T % DS) * kDstLevels * kTile, cy, DSCAN && !BT_ABL(g, 512),
-                                      (SEG || !kEmaNarrow) ? nullptr : nars + s);
+                                      (SEG || !kEmaNarrow) ? nullptr : nars + s, 0, 0, &inc2);
         const int pt = ring_pos(T, lane, R);
         r1[pt] = (uint64_t)pre;
-        const int64_t inc2 = wave_iscan_i64((int64_t)t * c);  // c = 0 past the end
         r2[pt] = cy2 + (uint64_t)inc2;
         cy2 += (uint64_t)lane63_i64(inc2);
     };

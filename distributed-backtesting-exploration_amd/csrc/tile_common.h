@@ -48,18 +48,28 @@ __device__ __forceinline__ uint32_t level_fill_slack(int32_t c, int32_t cp, int3
 // One whole wave, lane = bar t0 + lane, c = its close (0 past the end): writes the tile's
 // closes cT[64], the in-tile prefixes of the fixed-point returns ql[0..63] (q) and
 // ql[64..127] (q2), and the disjoint sparse table D[6][64] of the close path. Returns the
-// inclusive prefix sum of closes up to this lane's bar (exact int64). With HL, the bar's high
+// inclusive prefix sum of closes up to this lane's bar (exact int64); `also` (optional) is
+// replaced by its own inclusive wave prefix. AC: 64-bit scans as DPP add-with-carry pairs
+// (device_common.h wave_iscan_i64_ac). With HL, the bar's high
 // and low (hv, lv) add their level-fill slack to the narrow bound's total variation.
-template <bool HL = false>
+template <bool HL = false, bool AC = false>
 __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane, int32_t* cT,
                                              int64_t* ql, Agg* D, TileCarry& cy,
                                              bool with_dst = true, int32_t* narrow = nullptr,
-                                             int32_t hv = 0, int32_t lv = 0) {
+                                             int32_t hv = 0, int32_t lv = 0, int64_t* also = nullptr) {
     const int t = t0 + lane;
     const bool valid = t < B;
     const int32_t cp = (int32_t)__builtin_amdgcn_update_dpp((uint32_t)cy.prevc, (uint32_t)c,
                                                             0x138, 0xf, 0xf, false);  // wave_shr:1
-    const int64_t inc = wave_iscan_i64((int64_t)c);
+    // the closes' prefix (AC: with the add-with-carry scans, paired with the caller's `also`)
+    int64_t inc = (int64_t)c;
+    if (AC && also != nullptr)
+        wave_iscan2_i64_ac(inc, *also);
+    else if (AC)
+        inc = wave_iscan_i64_ac(inc);
+    else
+        inc = wave_iscan_i64(inc);
+    if (!AC && also != nullptr) *also = wave_iscan_i64(*also);
     const int64_t pre = cy.P + inc;
     cT[lane] = c;
     int64_t q = 0, q2 = 0;
@@ -70,8 +80,14 @@ __device__ __forceinline__ int64_t tile_scan(int32_t c, int B, int t0, int lane,
     }
     if (HL && narrow != nullptr && valid)  // dv < 2^31, twice the slack <= 2^27: no wrap
         dv += 2 * level_fill_slack(c, t >= 1 ? cp : c, hv, lv);
-    ql[lane] = wave_iscan_i64(q);
-    ql[kTile + lane] = wave_iscan_i64(q2);
+    if (AC) {
+        wave_iscan2_i64_ac(q, q2);
+    } else {
+        q = wave_iscan_i64(q);
+        q2 = wave_iscan_i64(q2);
+    }
+    ql[lane] = q;
+    ql[kTile + lane] = q2;
     if (narrow != nullptr) {  // the tile's total variation and the narrow flag (Acct32)
         const bool big = __ballot(dv >= (1u << 25)) != 0;
         const uint32_t tvt = __builtin_amdgcn_readlane(wave_iscan_u32(min(dv, 1u << 25)), 63);
