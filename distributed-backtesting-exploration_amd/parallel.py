@@ -96,11 +96,35 @@ def exchange_async(local: np.ndarray, k: int, counters, dist) -> PendingExchange
 
 def make_comm(dist, device: int, k: int):
     """The C-ABI exchange (engine.Comm over RCCL) for this process group: rank 0 creates the RCCL
-    unique id, the launcher's process group broadcasts it, every rank joins."""
-    from .engine import Comm
-    obj = [Comm.unique_id() if dist.get_rank() == 0 else None]
+    unique id, the launcher's process group broadcasts it, every rank joins. Every rank raises the
+    same BtError when rank 0 has no id (RCCL not loadable there), rather than ranks 1.. waiting in
+    the broadcast for a rank that gave up; and the ranks agree afterwards, so a rank whose join
+    failed makes every rank fall back together (bench.py: torch.distributed carrier)."""
+    import torch
+    from .engine import BtError, Comm
+    uid, why = None, ""
+    if dist.get_rank() == 0:
+        try:
+            uid = Comm.unique_id()
+        except Exception as e:  # noqa: BLE001 — reported on every rank below
+            why = str(e)
+    obj = [(uid, why)]
     dist.broadcast_object_list(obj, src=0)
-    return Comm(obj[0], dist.get_rank(), dist.get_world_size(), device, k)
+    uid, why = obj[0]
+    if uid is None:
+        raise BtError(f"no RCCL unique id on rank 0: {why}")
+    comm, why = None, ""
+    try:
+        comm = Comm(uid, dist.get_rank(), dist.get_world_size(), device, k)
+    except Exception as e:  # noqa: BLE001
+        why = str(e)
+    ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=_device_for(dist))
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if comm is not None:
+            comm.close()
+        raise BtError(f"RCCL communicator not created on every rank{': ' + why if why else ''}")
+    return comm
 
 
 def allreduce_counters(values, dist) -> list:

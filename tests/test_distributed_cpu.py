@@ -92,3 +92,71 @@ def test_shard_covers_every_symbol_once():
                 b, c = PAR.shard(n, world, r)
                 got += list(range(b, b + c))
             assert got == list(range(n))
+
+
+class _FakeComm:
+    """Stands in for engine.Comm in the failure tests (no GPU here): rank 0 has an id, rank
+    `fail_rank` cannot join."""
+    fail_rank = -1
+    closed = False
+
+    @staticmethod
+    def unique_id():
+        return b"\0" * 128
+
+    def __init__(self, uid, rank, world, device, k):
+        if rank == _FakeComm.fail_rank:
+            raise RuntimeError(f"rank {rank} cannot join")
+
+    def close(self):
+        _FakeComm.closed = True
+
+
+def _comm_worker(rank, world, port, q, mode):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "oracle"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from dbx_amd import engine as E
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        if mode == "no_id":      # rank 0 cannot produce the RCCL unique id
+            def no_id():
+                raise E.BtError("RCCL is not loadable")
+            E.Comm.unique_id = staticmethod(no_id)
+        else:                    # the last rank cannot join the communicator
+            _FakeComm.fail_rank = world - 1
+            E.Comm = _FakeComm
+        try:
+            PAR.make_comm(dist, 0, 5)
+            q.put((rank, "ok", False))
+        except E.BtError as e:
+            q.put((rank, str(e), _FakeComm.closed))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["no_id", "join_fails"])
+def test_make_comm_fails_on_every_rank_together(mode):
+    """bench.py falls back to the torch.distributed exchange when the C-ABI communicator cannot
+    be made; every rank must reach that decision (a rank left waiting in the id broadcast or in
+    the communicator's join would hang the run)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q, mode)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = "no RCCL unique id on rank 0" if mode == "no_id" else "not created on every rank"
+    for rank, msg, closed in out:
+        assert want in msg, (rank, msg)
+        if mode == "join_fails" and rank < world - 1:
+            assert closed, rank  # the ranks that had joined released their communicator
